@@ -1,0 +1,40 @@
+# Build: the product library (HIP for gfx950 + C++ host C-ABI) and the CPU oracle (test infra).
+#   make            -> both
+#   make lib        -> ssnt-tts-rust_amd/lib/libssnt_tts_c.so
+#   make oracle     -> oracle/build/libssnt_oracle.so
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+PKG       := ssnt-tts-rust_amd
+CSRC      := $(PKG)/csrc
+LIBDIR    := $(PKG)/lib
+LIB       := $(LIBDIR)/libssnt_tts_c.so
+ORACLE    := oracle/build/libssnt_oracle.so
+
+# -ffp-contract=off: the fwd-bwd arithmetic is specified op-by-op (no a*b+c contraction) so
+# the CPU oracle reproduces it bit for bit. Correctly rounded f32 division is HIP's default.
+HIPFLAGS  := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall \
+             -Wno-unused-function -I include -I $(CSRC)
+HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/decode.hip $(CSRC)/capi.hip
+HIP_HDRS  := $(wildcard $(CSRC)/*.h) include/ssnt_tts_c.h
+HIP_OBJS  := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(HIP_SRCS))
+
+all: lib oracle
+
+lib: $(LIB)
+oracle: $(ORACLE)
+
+$(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS)
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(HIP_OBJS) -Wl,-soname,libssnt_tts_c.so
+
+$(ORACLE): oracle/ssnt_oracle.c
+	@mkdir -p $(dir $@)
+	gcc -O3 -std=c11 -fopenmp -ffp-contract=off -fPIC -shared -Wall -o $@ $< -lm
+
+clean:
+	rm -rf $(LIBDIR) oracle/build
+
+.PHONY: all lib oracle clean

@@ -1,0 +1,195 @@
+/*
+ * ssnt_tts_c.h -- drop-in C ABI of libssnt_tts_c, MI355X (gfx950) implementation.
+ *
+ * Part 1 re-exports, with identical names, argument order, types and meaning, the seven
+ * unmangled symbols of the reference's Rust `staticlib` ssnt_tts_c
+ * (nii-yamagishilab/ssnt-tts-rust, ssnt_tts_c/src/lib.rs), which the TensorFlow custom ops in
+ * ssnt-tts-tensorflow/src/ (*_op.cc) declare `extern "C"` and link with -lssnt_tts_c
+ * (ssnt-tts-tensorflow/setup.py:15,40-42). Arguments are HOST pointers; each call is
+ * synchronous; contract violations print to stderr and abort(), as the Rust assert!/panic in
+ * an extern fn does. The work runs on the GPU (per-thread stream and scratch; reentrant).
+ *
+ * Part 2 adds entry points the reference does not have: the lattice forward-backward
+ * (SURVEY.md 8(a) A11), batched and fused decode, and device-pointer + hipStream_t variants of
+ * every kernel. They return an ssnt_status code instead of aborting.
+ *
+ * `bool` is the 1-byte C99/C++ bool, identical to Rust's `bool` in extern fns.
+ */
+#ifndef SSNT_TTS_C_H
+#define SSNT_TTS_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ===================== Part 1: reference symbols (host pointers) ===================== */
+
+/* One v1 emit/shift beam-search step, batch fixed to 1.
+ * Replaces ssnt_tts_c/src/lib.rs:11-83 (-> src/lib.rs:121-230); caller
+ * ssnt-tts-tensorflow/src/ssnt_tts_beam_search_decode_op.cc:5-8,116-128.
+ * h (W,2) [emit, shift] log-probs; log_prob_history, is_finished, t, u (W); outputs (W). */
+void ssnt_tts_beam_search_decode(const float *h, const float *log_prob_history,
+                                 const bool *is_finished, const int *t, const int *u, int max_t,
+                                 int beam_width, int *prediction, float *log_probs, int *next_t,
+                                 int *next_u, bool *next_is_finished, int *beam_branch);
+
+/* Backtrace of the best final beam. Replaces ssnt_tts_c/src/lib.rs:87-116
+ * (-> src/util.rs:20-33); caller ssnt_extract_best_beam_branch_op.cc:6-8 (declared `bool`
+ * there, return value ignored). beam_branch, t_history (max_u, W); outputs (max_u). */
+void ssnt_extract_best_beam_branch(int best_final_branch, const int *beam_branch,
+                                   const int *t_history, int beam_width, int max_u,
+                                   int *best_beam_branch, int *best_t_history);
+
+/* One v2 duration-class beam-search step. Replaces ssnt_tts_c/src/lib.rs:119-218
+ * (-> src/v2.rs:221-339); caller ssnt_tts_v2_beam_search_decode_op.cc:5-26,179-200.
+ * h (B,W,D); state (B,W); duration_table (D); input/output_length (B); outputs (B,W). */
+void ssnt_tts_v2_beam_search_decode(const float *h, const float *log_prob_history,
+                                    const bool *is_finished, const int *total_duration,
+                                    const int *duration_table, const int *t, const int *u,
+                                    const int *input_length, const int *output_length,
+                                    int batch_size, int beam_width, int duration_class_size,
+                                    int zero_duration_id, bool allow_skip, bool test_mode,
+                                    int *prediction, float *log_probs, int *next_t, int *next_u,
+                                    bool *next_is_finished, int *next_total_duration,
+                                    int *beam_branch);
+
+/* Backtrace of every final beam. Replaces ssnt_tts_c/src/lib.rs:221-241
+ * (-> src/v2_util.rs:6-36); caller ssnt_order_beam_branch_op.cc:6-11.
+ * final_branch (B,W); beam_branch (B,max_t,W); ordered_beam_branch (B,W,max_t). */
+void ssnt_order_beam_branch(const int *final_branch, const int *beam_branch, int batch_size,
+                            int beam_width, int max_t, int *ordered_beam_branch);
+
+/* Durations -> frame-to-input index map. Replaces ssnt_tts_c/src/lib.rs:245-265
+ * (-> src/v2_util.rs:39-66); caller upsample_source_indexes_op.cc:6-12. Writes only the first
+ * min(output_length[b,w], max_u) entries of each (b,w) row (the op prefills the rest). */
+void ssnt_upsample_source_indexes(const int *duration, const int *output_length, int batch_size,
+                                  int beam_width, int max_t, int max_u,
+                                  int *upsampled_source_indexes);
+
+/* One tone-latent beam-search step. Replaces ssnt_tts_c/src/lib.rs:268-343
+ * (-> src/tone_latent.rs:144-234); caller tone_latent_beam_search_decode_op.cc. */
+void tone_latent_beam_search_decode(const float *h, const float *log_prob_history,
+                                    const bool *is_finished, const int *t, const int *u,
+                                    const int *input_length, int batch_size, int beam_width,
+                                    int tone_class_size, int empty_tone_id, int *prediction,
+                                    float *log_probs, int *next_t, int *next_u,
+                                    bool *next_is_finished, int *beam_branch);
+
+/* Batched Levenshtein distance. Replaces ssnt_tts_c/src/lib.rs:347-381
+ * (-> src/edit_distance.rs:6-60); caller ssnt_tts_edit_distance.cc. */
+void tone_latent_levenshtein_edit_distance(const int *a, const int *b, const int *a_lengths,
+                                           const int *b_lengths, int batch_size,
+                                           int max_length, int *distance);
+
+/* ===================== Part 2: extensions ===================== */
+
+typedef enum {
+  SSNT_OK = 0,
+  SSNT_ERR_INVALID_ARG = 1,
+  SSNT_ERR_HIP = 2,
+  SSNT_ERR_NO_CANDIDATE = 3,      /* v2: src/v2.rs:292 assert */
+  SSNT_ERR_DURATION_MISMATCH = 4, /* upsample: src/v2_util.rs:58 assert */
+  SSNT_ERR_UNSUPPORTED = 5,       /* size outside what the kernels handle */
+  SSNT_ERR_WORKSPACE = 6,         /* workspace missing / too small */
+  SSNT_ERR_BAD_LENGTH = 7,        /* a length exceeds the tensor extent */
+  SSNT_ERR_BAD_INDEX = 8          /* backtrace branch index outside [0, W) */
+} ssnt_status;
+
+const char *ssnt_status_string(int status);
+/* translate the bits a kernel OR-ed into a device status word into an ssnt_status */
+int ssnt_status_from_bits(int bits);
+/* library / device info: fills a short human-readable string, returns SSNT_OK */
+int ssnt_version(char *buf, size_t len);
+
+/* lattice flags */
+#define SSNT_FLAG_TERMINAL_EMIT 1 /* Z includes the terminal emit at (S-1,P-1) (src/lib.rs:187-195) */
+#define SSNT_FLAG_ZERO_INFINITY 2 /* infeasible utterances report loss 0 instead of +inf */
+
+/* ---- emit/shift lattice forward-backward ----
+ * log_trans (B,T,U,2) f32 natural-log [emit, shift] probabilities, row-major;
+ * log_obs (B,T,U) optional per-cell log-likelihood (NULL = none);
+ * step_len, pos_len (B): lattice extent S_b <= T steps, P_b <= U positions.
+ * Outputs: loss (B) = -ln Z; grad_trans (B,T,U,2) = d loss / d log_trans (NULL = skip);
+ * grad_obs (B,T,U) = d loss / d log_obs (NULL = skip); log_alpha / log_beta (B,T,U) debug
+ * outputs (NULL = skip). Cells outside (S_b,P_b) get grad 0 and log-alpha/beta -inf.
+ * Device variant: all pointers are device pointers; `stream` is a hipStream_t (NULL = legacy
+ * default); `workspace` must hold ssnt_fwd_bwd_workspace_size() bytes (may be 0 -> NULL);
+ * `status` (device int, may be NULL) receives error bits. Asynchronous. */
+size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos);
+int ssnt_fwd_bwd_device(const float *log_trans, const float *log_obs, const int *step_len,
+                        const int *pos_len, int batch, int max_steps, int max_pos, int flags,
+                        float *loss, float *grad_trans, float *grad_obs, float *log_alpha,
+                        float *log_beta, void *workspace, size_t workspace_bytes, int *status,
+                        void *stream);
+/* Host-pointer variant (synchronous; copies through the calling thread's GPU context). */
+int ssnt_fwd_bwd(const float *log_trans, const float *log_obs, const int *step_len,
+                 const int *pos_len, int batch, int max_steps, int max_pos, int flags,
+                 float *loss, float *grad_trans, float *grad_obs, float *log_alpha,
+                 float *log_beta);
+
+/* ---- batched decode steps, device pointers (the reference FFI fixes v1 to B=1,
+ * ssnt_tts_c/src/lib.rs:13; its Rust API takes B, src/lib.rs:121). max_beam_width = beam_width
+ * as in every reference call site (ssnt_tts_c/src/lib.rs:82,217,342). ---- */
+int ssnt_beam_search_decode_device(const float *h, const float *log_prob_history,
+                                   const bool *is_finished, const int *t, const int *u,
+                                   const int *input_length, int batch_size, int beam_width,
+                                   int *prediction, float *log_probs, int *next_t, int *next_u,
+                                   bool *next_is_finished, int *beam_branch, int *status,
+                                   void *stream);
+int ssnt_v2_beam_search_decode_device(const float *h, const float *log_prob_history,
+                                      const bool *is_finished, const int *total_duration,
+                                      const int *duration_table, const int *t, const int *u,
+                                      const int *input_length, const int *output_length,
+                                      int batch_size, int beam_width, int duration_class_size,
+                                      int zero_duration_id, bool allow_skip, bool test_mode,
+                                      int *prediction, float *log_probs, int *next_t,
+                                      int *next_u, bool *next_is_finished,
+                                      int *next_total_duration, int *beam_branch, int *status,
+                                      void *stream);
+int ssnt_tone_latent_beam_search_decode_device(const float *h, const float *log_prob_history,
+                                               const bool *is_finished, const int *t,
+                                               const int *u, const int *input_length,
+                                               int batch_size, int beam_width,
+                                               int tone_class_size, int empty_tone_id,
+                                               int *prediction, float *log_probs, int *next_t,
+                                               int *next_u, bool *next_is_finished,
+                                               int *beam_branch, int *status, void *stream);
+
+/* Fused T-step v1 decode over a (B,T,U,2) log-prob lattice: step s feeds each beam
+ * h = lattice[b, u, t, :]; all beams start at t=u=0, log-prob 0. Per-step outputs (B,T,W);
+ * best_beam_branch / best_t_history (B,T) = backtrace of slot 0 after the last step with
+ * t_history = next_t (src/util.rs:20-33). */
+int ssnt_lattice_beam_search_decode_device(const float *lattice, const int *input_length,
+                                           int batch_size, int max_steps, int max_pos,
+                                           int beam_width, int *prediction, float *log_probs,
+                                           int *next_t, int *next_u, bool *next_is_finished,
+                                           int *beam_branch, int *best_beam_branch,
+                                           int *best_t_history, int *status, void *stream);
+
+/* Batched backtraces / utilities, device pointers. */
+int ssnt_extract_best_beam_branch_device(const int *best_final_branch, const int *beam_branch,
+                                         const int *t_history, int batch_size, int beam_width,
+                                         int max_u, int *best_beam_branch, int *best_t_history,
+                                         int *status, void *stream);
+int ssnt_order_beam_branch_device(const int *final_branch, const int *beam_branch,
+                                  int batch_size, int beam_width, int max_t,
+                                  int *ordered_beam_branch, int *status, void *stream);
+int ssnt_upsample_source_indexes_device(const int *duration, const int *output_length,
+                                        int batch_size, int beam_width, int max_t, int max_u,
+                                        int *upsampled_source_indexes, int *status,
+                                        void *stream);
+int ssnt_levenshtein_edit_distance_device(const int *a, const int *b, const int *a_lengths,
+                                          const int *b_lengths, int batch_size, int max_length,
+                                          int *distance, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SSNT_TTS_C_H */

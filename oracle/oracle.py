@@ -1,0 +1,247 @@
+"""CPU oracle loader -- TEST INFRASTRUCTURE ONLY.
+
+Loads ``oracle/build/libssnt_oracle.so`` (built from ``oracle/ssnt_oracle.c`` by ``make oracle``)
+and exposes numpy-in / numpy-out wrappers. Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module; the product package
+(``ssnt-tts-rust_amd/``) never does. See ``oracle/ssnt_oracle.c`` for the reference citations.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+_LIB_PATH = _HERE / "build" / "libssnt_oracle.so"
+_lib = None
+
+FLAG_TERMINAL_EMIT = 1
+FLAG_ZERO_INFINITY = 2
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_boolp = ctypes.POINTER(ctypes.c_bool)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise RuntimeError(f"oracle not built: {_LIB_PATH} (run `make oracle`)")
+        _lib = ctypes.CDLL(str(_LIB_PATH))
+    return _lib
+
+
+def _p(a, kind):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "oracle inputs must be C-contiguous"
+    return a.ctypes.data_as(kind)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _b(a):
+    return np.ascontiguousarray(a, dtype=np.bool_)
+
+
+def v1_step(h, hist, fin, t, u, input_length, max_beam_width=None):
+    """Batched v1 step (src/lib.rs:121-230). h (B,W,2); state (B,W); input_length (B,)."""
+    h = _f32(h)
+    B, W, _ = h.shape
+    Wm = W if max_beam_width is None else max_beam_width
+    outs = dict(
+        prediction=np.zeros((B, Wm), np.int32), log_prob=np.zeros((B, Wm), np.float32),
+        next_t=np.zeros((B, Wm), np.int32), next_u=np.zeros((B, Wm), np.int32),
+        next_is_finished=np.zeros((B, Wm), np.bool_), beam_branch=np.zeros((B, Wm), np.int32))
+    L = lib()
+    rc = L.oracle_v1_step(
+        B, W, Wm, _p(h, _f32p), _p(_f32(hist), _f32p), _p(_b(fin), _boolp), _p(_i32(t), _i32p),
+        _p(_i32(u), _i32p), _p(_i32(input_length), _i32p), _p(outs["prediction"], _i32p),
+        _p(outs["log_prob"], _f32p), _p(outs["next_t"], _i32p), _p(outs["next_u"], _i32p),
+        _p(outs["next_is_finished"], _boolp), _p(outs["beam_branch"], _i32p))
+    if rc != 0:
+        raise RuntimeError(f"oracle_v1_step status {rc}")
+    return outs
+
+
+def v2_step(h, hist, fin, total, table, t, u, input_length, output_length, zero_duration_id,
+            allow_skip, test_mode, max_beam_width=None):
+    """Batched v2 step (src/v2.rs:221-339). Returns (outs, status)."""
+    h = _f32(h)
+    B, W, D = h.shape
+    Wm = W if max_beam_width is None else max_beam_width
+    outs = dict(
+        prediction=np.zeros((B, Wm), np.int32), log_prob=np.zeros((B, Wm), np.float32),
+        next_t=np.zeros((B, Wm), np.int32), next_u=np.zeros((B, Wm), np.int32),
+        next_is_finished=np.zeros((B, Wm), np.bool_),
+        next_total_duration=np.zeros((B, Wm), np.int32), beam_branch=np.zeros((B, Wm), np.int32))
+    rc = lib().oracle_v2_step(
+        B, W, Wm, D, _p(h, _f32p), _p(_f32(hist), _f32p), _p(_b(fin), _boolp),
+        _p(_i32(total), _i32p), _p(_i32(table), _i32p), _p(_i32(t), _i32p), _p(_i32(u), _i32p),
+        _p(_i32(input_length), _i32p), _p(_i32(output_length), _i32p), int(zero_duration_id),
+        ctypes.c_bool(allow_skip), ctypes.c_bool(test_mode), _p(outs["prediction"], _i32p),
+        _p(outs["log_prob"], _f32p), _p(outs["next_t"], _i32p), _p(outs["next_u"], _i32p),
+        _p(outs["next_is_finished"], _boolp), _p(outs["next_total_duration"], _i32p),
+        _p(outs["beam_branch"], _i32p))
+    return outs, rc
+
+
+def tone_step(h, hist, fin, t, u, input_length, empty_tone_id, max_beam_width=None):
+    """Batched tone-latent step (src/tone_latent.rs:144-234)."""
+    h = _f32(h)
+    B, W, C = h.shape
+    Wm = W if max_beam_width is None else max_beam_width
+    outs = dict(
+        prediction=np.zeros((B, Wm), np.int32), log_prob=np.zeros((B, Wm), np.float32),
+        next_t=np.zeros((B, Wm), np.int32), next_u=np.zeros((B, Wm), np.int32),
+        next_is_finished=np.zeros((B, Wm), np.bool_), beam_branch=np.zeros((B, Wm), np.int32))
+    rc = lib().oracle_tone_step(
+        B, W, Wm, C, _p(h, _f32p), _p(_f32(hist), _f32p), _p(_b(fin), _boolp),
+        _p(_i32(t), _i32p), _p(_i32(u), _i32p), _p(_i32(input_length), _i32p),
+        int(empty_tone_id), _p(outs["prediction"], _i32p), _p(outs["log_prob"], _f32p),
+        _p(outs["next_t"], _i32p), _p(outs["next_u"], _i32p),
+        _p(outs["next_is_finished"], _boolp), _p(outs["beam_branch"], _i32p))
+    if rc != 0:
+        raise RuntimeError(f"oracle_tone_step status {rc}")
+    return outs
+
+
+def extract_best_beam_branch(best_final_branch, beam_branch, t_history):
+    """util::extract_best_beam_branch_kernel (src/util.rs:20-33); beam_branch (U,W)."""
+    bb = _i32(beam_branch)
+    th = _i32(t_history)
+    U, W = bb.shape
+    out = np.zeros(U, np.int32)
+    out_t = np.zeros(U, np.int32)
+    lib().oracle_extract_best_beam_branch(int(best_final_branch), _p(bb, _i32p), _p(th, _i32p),
+                                          W, U, _p(out, _i32p), _p(out_t, _i32p))
+    return out, out_t
+
+
+def order_beam_branch(final_branch, beam_branch):
+    """v2_util::order_beam_branch (src/v2_util.rs:6-36): (B,W),(B,T,W) -> (B,W,T)."""
+    fb = _i32(final_branch)
+    bb = _i32(beam_branch)
+    B, T, W = bb.shape
+    out = np.zeros((B, W, T), np.int32)
+    lib().oracle_order_beam_branch(B, W, T, _p(fb, _i32p), _p(bb, _i32p), _p(out, _i32p))
+    return out
+
+
+def upsample_source_indexes(duration, output_length, max_u, fill=-1):
+    """v2_util::upsample_source_indexes (src/v2_util.rs:39-66) + the TF op prefill."""
+    d = _i32(duration)
+    B, W, T = d.shape
+    out = np.full((B, W, max_u), fill, np.int32)
+    rc = lib().oracle_upsample_source_indexes(B, W, T, int(max_u), _p(d, _i32p),
+                                              _p(_i32(output_length), _i32p), _p(out, _i32p))
+    return out, rc
+
+
+def levenshtein(a, b, a_len, b_len):
+    """edit_distance::levenshtein_edit_distance (src/edit_distance.rs:6-31)."""
+    a = _i32(a)
+    b = _i32(b)
+    B, L = a.shape
+    out = np.zeros(B, np.int32)
+    lib().oracle_levenshtein(B, L, _p(a, _i32p), _p(b, _i32p), _p(_i32(a_len), _i32p),
+                             _p(_i32(b_len), _i32p), _p(out, _i32p))
+    return out
+
+
+def v1_lattice_decode(lattice, input_length, beam_width, n_threads=0):
+    """Fused multi-step v1 decode over a (B,T,U,2) lattice (config 3 workload)."""
+    lat = _f32(lattice)
+    B, T, U, _ = lat.shape
+    W = beam_width
+    o = dict(prediction=np.zeros((B, T, W), np.int32), log_prob=np.zeros((B, T, W), np.float32),
+             next_t=np.zeros((B, T, W), np.int32), next_u=np.zeros((B, T, W), np.int32),
+             next_is_finished=np.zeros((B, T, W), np.bool_),
+             beam_branch=np.zeros((B, T, W), np.int32),
+             best_beam_branch=np.zeros((B, T), np.int32),
+             best_t_history=np.zeros((B, T), np.int32))
+    rc = lib().oracle_v1_lattice_decode(
+        B, T, U, W, _p(lat, _f32p), _p(_i32(input_length), _i32p), _p(o["prediction"], _i32p),
+        _p(o["log_prob"], _f32p), _p(o["next_t"], _i32p), _p(o["next_u"], _i32p),
+        _p(o["next_is_finished"], _boolp), _p(o["beam_branch"], _i32p),
+        _p(o["best_beam_branch"], _i32p), _p(o["best_t_history"], _i32p), int(n_threads))
+    if rc != 0:
+        raise RuntimeError(f"oracle_v1_lattice_decode status {rc}")
+    return o
+
+
+def fwd_bwd_xf(log_trans, step_len, pos_len, log_obs=None, flags=FLAG_TERMINAL_EMIT,
+               debug=False, n_threads=0):
+    """Exact split-exponent f32 fwd-bwd (the arithmetic the HIP kernel reproduces bit-exactly)."""
+    lt = _f32(log_trans)
+    B, T, U, _ = lt.shape
+    lo = None if log_obs is None else _f32(log_obs)
+    loss = np.zeros(B, np.float32)
+    grad = np.zeros((B, T, U, 2), np.float32)
+    gobs = None if lo is None else np.zeros((B, T, U), np.float32)
+    la = np.zeros((B, T, U), np.float32) if debug else None
+    lb = np.zeros((B, T, U), np.float32) if debug else None
+    lib().oracle_fwd_bwd_xf(B, T, U, _p(lt, _f32p), _p(lo, _f32p), _p(_i32(step_len), _i32p),
+                            _p(_i32(pos_len), _i32p), int(flags), _p(loss, _f32p),
+                            _p(grad, _f32p), _p(gobs, _f32p), _p(la, _f32p), _p(lb, _f32p),
+                            int(n_threads))
+    out = dict(loss=loss, grad=grad)
+    if gobs is not None:
+        out["grad_obs"] = gobs
+    if debug:
+        out["log_alpha"] = la
+        out["log_beta"] = lb
+    return out
+
+
+def fwd_bwd_f64(log_trans, step_len, pos_len, log_obs=None, flags=FLAG_TERMINAL_EMIT):
+    """Independent float64 log-domain DP: the mathematical definition of the lattice."""
+    lt = _f32(log_trans)
+    B, T, U, _ = lt.shape
+    lo = None if log_obs is None else _f32(log_obs)
+    loss = np.zeros(B, np.float64)
+    grad = np.zeros((B, T, U, 2), np.float64)
+    gobs = None if lo is None else np.zeros((B, T, U), np.float64)
+    la = np.zeros((B, T, U), np.float64)
+    lb = np.zeros((B, T, U), np.float64)
+    lib().oracle_fwd_bwd_f64(B, T, U, _p(lt, _f32p), _p(lo, _f32p), _p(_i32(step_len), _i32p),
+                             _p(_i32(pos_len), _i32p), int(flags), _p(loss, _f64p),
+                             _p(grad, _f64p), _p(gobs, _f64p), _p(la, _f64p), _p(lb, _f64p))
+    out = dict(loss=loss, grad=grad, log_alpha=la, log_beta=lb)
+    if gobs is not None:
+        out["grad_obs"] = gobs
+    return out
+
+
+def max_threads():
+    return int(lib().oracle_omp_max_threads())
+
+
+# ---- synthetic inputs shared by tests and bench (counter-based, reproducible) ----------------
+def synth_log_trans(B, T, U, seed=0, scale=1.5):
+    """log_softmax over k of z ~ N(0, scale^2), f32, shape (B,T,U,2)."""
+    rng = np.random.default_rng(seed)
+    z = rng.standard_normal((B, T, U, 2), dtype=np.float32) * np.float32(scale)
+    m = z.max(axis=-1, keepdims=True)
+    lse = m + np.log(np.exp(z - m).sum(axis=-1, keepdims=True))
+    return (z - lse).astype(np.float32)
+
+
+def synth_tie_rich_log_trans(B, T, U, seed=0):
+    """Tie-rich lattice: p in {0.1,...,0.9}, ln in f32, like the reference tests
+    (tests/test_decoding.rs:8, ssnt-tts-tensorflow/tests/test_beam_search_op.py:37-38)."""
+    rng = np.random.default_rng(seed)
+    p = (rng.integers(1, 10, size=(B, T, U, 1)) / 10.0).astype(np.float32)
+    pe = p
+    ps = (np.float32(1.0) - p).astype(np.float32)
+    return np.log(np.concatenate([pe, ps], axis=-1).astype(np.float32)).astype(np.float32)

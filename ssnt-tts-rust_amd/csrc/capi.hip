@@ -1,0 +1,635 @@
+// capi.hip -- host side of libssnt_tts_c: the reference's seven extern "C" symbols (host
+// pointers, synchronous, abort on contract violation) and the device-pointer extensions.
+//
+// Reference symbols (ssnt_tts_c/src/lib.rs) take host arrays owned by the TF op for the call
+// only. Each call here packs its inputs into one pinned staging buffer, does
+// one H2D copy, launches the HIP kernel(s) and one D2H copy on the calling thread's own stream,
+// then synchronises. Streams and scratch are thread_local: TF calls ops from several inter-op
+// threads concurrently and the calls share nothing.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "ssnt_internal.h"
+
+namespace ssnt {
+
+int status_bits_to_code(int bits) {
+  if (bits & kStatusNoCandidate) return SSNT_ERR_NO_CANDIDATE;
+  if (bits & kStatusDurationMismatch) return SSNT_ERR_DURATION_MISMATCH;
+  if (bits & kStatusBadLength) return SSNT_ERR_BAD_LENGTH;
+  if (bits & kStatusBadIndex) return SSNT_ERR_BAD_INDEX;
+  return SSNT_OK;
+}
+
+namespace {
+
+[[noreturn]] void fail(const char* fn, const char* msg) {
+  // mirrors a Rust panic escaping an extern fn: the process aborts
+  fprintf(stderr, "libssnt_tts_c: %s: %s\n", fn, msg);
+  fflush(stderr);
+  abort();
+}
+
+void check_ptr(const void* p, const char* fn, const char* name) {
+  if (p == nullptr) {
+    char buf[128];
+    snprintf(buf, sizeof buf, "assertion failed: !%s.is_null()", name);
+    fail(fn, buf);
+  }
+}
+
+// Per-thread GPU context: stream, device scratch, pinned staging, status word.
+struct HostCtx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  char* d = nullptr;
+  size_t dcap = 0;
+  char* h = nullptr;
+  size_t hcap = 0;
+};
+thread_local HostCtx g_ctx;
+
+int ctx_ready(const char* fn, bool abort_on_error) {
+  int dev = -1;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    if (abort_on_error) fail(fn, "no HIP device available (libssnt_tts_c has no CPU fallback)");
+    return SSNT_ERR_HIP;
+  }
+  if (hipGetDevice(&dev) != hipSuccess) {
+    if (abort_on_error) fail(fn, "hipGetDevice failed");
+    return SSNT_ERR_HIP;
+  }
+  if (g_ctx.device != dev) {
+    // a different device for this thread: drop old resources (they belong to another device)
+    g_ctx = HostCtx{};
+    g_ctx.device = dev;
+    if (hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking) != hipSuccess) {
+      if (abort_on_error) fail(fn, "hipStreamCreate failed");
+      return SSNT_ERR_HIP;
+    }
+  }
+  return SSNT_OK;
+}
+
+int ensure(size_t dbytes, size_t hbytes, const char* fn, bool abort_on_error) {
+  if (dbytes > g_ctx.dcap) {
+    if (g_ctx.d) {
+      (void)hipStreamSynchronize(g_ctx.stream);
+      (void)hipFree(g_ctx.d);
+    }
+    g_ctx.d = nullptr;
+    g_ctx.dcap = 0;
+    const size_t cap = dbytes + dbytes / 2 + 4096;
+    if (hipMalloc(reinterpret_cast<void**>(&g_ctx.d), cap) != hipSuccess) {
+      if (abort_on_error) fail(fn, "hipMalloc failed");
+      return SSNT_ERR_HIP;
+    }
+    g_ctx.dcap = cap;
+  }
+  if (hbytes > g_ctx.hcap) {
+    if (g_ctx.h) {
+      (void)hipStreamSynchronize(g_ctx.stream);
+      (void)hipHostFree(g_ctx.h);
+    }
+    g_ctx.h = nullptr;
+    g_ctx.hcap = 0;
+    const size_t cap = hbytes + hbytes / 2 + 4096;
+    if (hipHostMalloc(reinterpret_cast<void**>(&g_ctx.h), cap, hipHostMallocDefault) != hipSuccess) {
+      if (abort_on_error) fail(fn, "hipHostMalloc failed");
+      return SSNT_ERR_HIP;
+    }
+    g_ctx.hcap = cap;
+  }
+  return SSNT_OK;
+}
+
+// Staging plan: a list of host arrays laid out in one buffer (inputs first, then outputs).
+struct Slot {
+  const void* src;  // host input (null for pure outputs)
+  void* dst;        // host output (null for pure inputs)
+  size_t bytes;
+  size_t off;
+};
+
+struct Plan {
+  std::vector<Slot> in, out;
+  size_t in_bytes = 0, total = 0;
+  static size_t align(size_t x) { return (x + 255) & ~size_t(255); }
+  int add_in(const void* src, size_t bytes) {
+    in.push_back(Slot{src, nullptr, bytes, 0});
+    return (int)in.size() - 1;
+  }
+  int add_out(void* dst, size_t bytes, const void* init = nullptr) {
+    out.push_back(Slot{init, dst, bytes, 0});
+    return (int)out.size() - 1;
+  }
+  void layout() {
+    size_t o = 0;
+    for (auto& s : in) { s.off = o; o += align(s.bytes); }
+    // outputs that need their previous contents (init) are uploaded too
+    for (auto& s : out) { s.off = o; o += align(s.bytes); }
+    in_bytes = o;
+    total = o + 256;  // + status word
+  }
+  template <typename T> T* din(int i) const { return reinterpret_cast<T*>(g_ctx.d + in[i].off); }
+  template <typename T> T* dout(int i) const { return reinterpret_cast<T*>(g_ctx.d + out[i].off); }
+  int* dstatus() const { return reinterpret_cast<int*>(g_ctx.d + in_bytes); }
+};
+
+// Upload inputs (and output init contents), zero the status word.
+int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device = 0) {
+  p.layout();
+  int rc = ensure(Plan::align(p.total) + extra_device, p.total, fn, abort_on_error);
+  if (rc != SSNT_OK) return rc;
+  for (auto& s : p.in) memcpy(g_ctx.h + s.off, s.src, s.bytes);
+  size_t up_end = 0;
+  for (auto& s : p.in) up_end = s.off + s.bytes;
+  for (auto& s : p.out)
+    if (s.src) {
+      memcpy(g_ctx.h + s.off, s.src, s.bytes);
+      up_end = s.off + s.bytes;
+    }
+  memset(g_ctx.h + p.in_bytes, 0, sizeof(int));
+  hipError_t e = hipSuccess;
+  if (up_end) e = hipMemcpyAsync(g_ctx.d, g_ctx.h, up_end, hipMemcpyHostToDevice, g_ctx.stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(g_ctx.d + p.in_bytes, g_ctx.h + p.in_bytes, sizeof(int),
+                       hipMemcpyHostToDevice, g_ctx.stream);
+  if (e != hipSuccess) {
+    if (abort_on_error) fail(fn, hipGetErrorString(e));
+    return SSNT_ERR_HIP;
+  }
+  return SSNT_OK;
+}
+
+// Download outputs + status, synchronise, scatter to the caller's arrays. Returns status code.
+int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
+  if (launch_rc != SSNT_OK) {
+    if (abort_on_error) fail(fn, ssnt_status_string(launch_rc));
+    return launch_rc;
+  }
+  size_t lo = p.in_bytes, hi = p.in_bytes + sizeof(int);
+  for (auto& s : p.out) {
+    lo = std::min(lo, s.off);
+    hi = std::max(hi, s.off + s.bytes);
+  }
+  hipError_t e = hipMemcpyAsync(g_ctx.h + lo, g_ctx.d + lo, hi - lo, hipMemcpyDeviceToHost, g_ctx.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(g_ctx.stream);
+  if (e != hipSuccess) {
+    if (abort_on_error) fail(fn, hipGetErrorString(e));
+    return SSNT_ERR_HIP;
+  }
+  int bits = 0;
+  memcpy(&bits, g_ctx.h + p.in_bytes, sizeof(int));
+  const int rc = status_bits_to_code(bits);
+  if (rc != SSNT_OK) {
+    if (abort_on_error) {
+      if (rc == SSNT_ERR_NO_CANDIDATE)
+        fail(fn, "assertion failed: Beam search could not find a duration sequence with "
+                 "compatible output length. Please increase duration class size and beam width.");
+      if (rc == SSNT_ERR_DURATION_MISMATCH)
+        fail(fn, "assertion failed: `(left == right)`: upsampled.len() != output_length");
+      fail(fn, ssnt_status_string(rc));
+    }
+    return rc;
+  }
+  for (auto& s : p.out) memcpy(s.dst, g_ctx.h + s.off, s.bytes);
+  return SSNT_OK;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+}  // namespace ssnt
+
+using namespace ssnt;
+
+extern "C" {
+
+const char* ssnt_status_string(int status) {
+  switch (status) {
+    case SSNT_OK: return "ok";
+    case SSNT_ERR_INVALID_ARG: return "invalid argument";
+    case SSNT_ERR_HIP: return "HIP runtime error";
+    case SSNT_ERR_NO_CANDIDATE: return "v2 beam search found no candidate (src/v2.rs:292)";
+    case SSNT_ERR_DURATION_MISMATCH: return "duration sum != output_length (src/v2_util.rs:58)";
+    case SSNT_ERR_UNSUPPORTED: return "size not supported by the kernels";
+    case SSNT_ERR_WORKSPACE: return "workspace missing or too small";
+    case SSNT_ERR_BAD_LENGTH: return "length exceeds tensor extent";
+    case SSNT_ERR_BAD_INDEX: return "beam branch index out of range";
+    default: return "unknown status";
+  }
+}
+
+int ssnt_status_from_bits(int bits) { return status_bits_to_code(bits); }
+
+int ssnt_version(char* buf, size_t len) {
+  if (buf && len) snprintf(buf, len, "libssnt_tts_c mi355x gfx950 (HIP %d.%d)", HIP_VERSION_MAJOR, HIP_VERSION_MINOR);
+  return SSNT_OK;
+}
+
+// ------------------------------- reference symbols -------------------------------------------
+
+void ssnt_tts_beam_search_decode(const float* h, const float* log_prob_history,
+                                 const bool* is_finished, const int* t, const int* u, int max_t,
+                                 int beam_width, int* prediction, float* log_probs, int* next_t,
+                                 int* next_u, bool* next_is_finished, int* beam_branch) {
+  static const char* fn = "ssnt_tts_beam_search_decode";
+  check_ptr(h, fn, "h"); check_ptr(log_prob_history, fn, "log_prob_history");
+  check_ptr(is_finished, fn, "is_finished"); check_ptr(t, fn, "t"); check_ptr(u, fn, "u");
+  check_ptr(prediction, fn, "prediction"); check_ptr(log_probs, fn, "log_probs");
+  check_ptr(next_t, fn, "next_t"); check_ptr(next_u, fn, "next_u");
+  check_ptr(next_is_finished, fn, "next_is_finished"); check_ptr(beam_branch, fn, "beam_branch");
+  if (beam_width <= 0) fail(fn, "chunk size must be non-zero (beam_width <= 0)");
+  ctx_ready(fn, true);
+  const size_t W = beam_width;
+  Plan p;
+  const int ih = p.add_in(h, W * 2 * 4), ihist = p.add_in(log_prob_history, W * 4),
+            ifin = p.add_in(is_finished, W), it = p.add_in(t, W * 4), iu = p.add_in(u, W * 4);
+  const int op = p.add_out(prediction, W * 4), ol = p.add_out(log_probs, W * 4),
+            ot = p.add_out(next_t, W * 4), ou = p.add_out(next_u, W * 4),
+            of = p.add_out(next_is_finished, W), ob = p.add_out(beam_branch, W * 4);
+  stage_in(p, fn, true);
+  StepArgs a{};
+  a.variant = Variant::V1;
+  a.B = 1; a.W = beam_width; a.Wmax = beam_width; a.C = 2;
+  a.h = p.din<float>(ih); a.hist = p.din<float>(ihist); a.fin = p.din<bool>(ifin);
+  a.t = p.din<int>(it); a.u = p.din<int>(iu);
+  a.input_length = nullptr; a.scalar_input_length = max_t;
+  a.prediction = p.dout<int>(op); a.log_prob = p.dout<float>(ol); a.next_t = p.dout<int>(ot);
+  a.next_u = p.dout<int>(ou); a.next_fin = p.dout<bool>(of); a.beam_branch = p.dout<int>(ob);
+  a.status = p.dstatus();
+  stage_out(p, launch_decode_step(a, g_ctx.stream), fn, true);
+}
+
+void ssnt_extract_best_beam_branch(int best_final_branch, const int* beam_branch,
+                                   const int* t_history, int beam_width, int max_u,
+                                   int* best_beam_branch, int* best_t_history) {
+  static const char* fn = "ssnt_extract_best_beam_branch";
+  check_ptr(beam_branch, fn, "beam_branch"); check_ptr(t_history, fn, "t_history");
+  check_ptr(best_beam_branch, fn, "best_beam_branch");
+  check_ptr(best_t_history, fn, "best_t_history");
+  if (beam_width <= 0 || max_u < 0) fail(fn, "chunk size must be non-zero (beam_width <= 0)");
+  if (max_u == 0) return;
+  ctx_ready(fn, true);
+  const size_t n = (size_t)max_u * beam_width;
+  Plan p;
+  const int ifb = p.add_in(&best_final_branch, 4), ib = p.add_in(beam_branch, n * 4),
+            ith = p.add_in(t_history, n * 4);
+  const int ob = p.add_out(best_beam_branch, (size_t)max_u * 4),
+            ot = p.add_out(best_t_history, (size_t)max_u * 4);
+  stage_in(p, fn, true);
+  const int rc = launch_extract_best(1, beam_width, max_u, p.din<int>(ifb), p.din<int>(ib),
+                                     p.din<int>(ith), p.dout<int>(ob), p.dout<int>(ot),
+                                     p.dstatus(), g_ctx.stream);
+  stage_out(p, rc, fn, true);
+}
+
+void ssnt_tts_v2_beam_search_decode(const float* h, const float* log_prob_history,
+                                    const bool* is_finished, const int* total_duration,
+                                    const int* duration_table, const int* t, const int* u,
+                                    const int* input_length, const int* output_length,
+                                    int batch_size, int beam_width, int duration_class_size,
+                                    int zero_duration_id, bool allow_skip, bool test_mode,
+                                    int* prediction, float* log_probs, int* next_t, int* next_u,
+                                    bool* next_is_finished, int* next_total_duration,
+                                    int* beam_branch) {
+  static const char* fn = "ssnt_tts_v2_beam_search_decode";
+  check_ptr(h, fn, "h"); check_ptr(log_prob_history, fn, "log_prob_history");
+  check_ptr(is_finished, fn, "is_finished"); check_ptr(total_duration, fn, "total_duration");
+  check_ptr(duration_table, fn, "duration_table"); check_ptr(t, fn, "t"); check_ptr(u, fn, "u");
+  check_ptr(input_length, fn, "input_length"); check_ptr(output_length, fn, "output_length");
+  check_ptr(prediction, fn, "prediction"); check_ptr(log_probs, fn, "log_probs");
+  check_ptr(next_t, fn, "next_t"); check_ptr(next_u, fn, "next_u");
+  check_ptr(next_is_finished, fn, "next_is_finished");
+  check_ptr(next_total_duration, fn, "next_total_duration");
+  check_ptr(beam_branch, fn, "beam_branch");
+  if (batch_size < 0 || beam_width <= 0 || duration_class_size <= 0)
+    fail(fn, "chunk size must be non-zero (beam_width / duration_class_size <= 0)");
+  if (batch_size == 0) return;
+  ctx_ready(fn, true);
+  const size_t BW = (size_t)batch_size * beam_width, D = duration_class_size;
+  Plan p;
+  const int ih = p.add_in(h, BW * D * 4), ihist = p.add_in(log_prob_history, BW * 4),
+            ifin = p.add_in(is_finished, BW), itot = p.add_in(total_duration, BW * 4),
+            itab = p.add_in(duration_table, D * 4), it = p.add_in(t, BW * 4),
+            iu = p.add_in(u, BW * 4), iil = p.add_in(input_length, (size_t)batch_size * 4),
+            iol = p.add_in(output_length, (size_t)batch_size * 4);
+  const int op = p.add_out(prediction, BW * 4), ol = p.add_out(log_probs, BW * 4),
+            ot = p.add_out(next_t, BW * 4), ou = p.add_out(next_u, BW * 4),
+            of = p.add_out(next_is_finished, BW), otd = p.add_out(next_total_duration, BW * 4),
+            ob = p.add_out(beam_branch, BW * 4);
+  stage_in(p, fn, true);
+  StepArgs a{};
+  a.variant = Variant::V2;
+  a.B = batch_size; a.W = beam_width; a.Wmax = beam_width; a.C = duration_class_size;
+  a.h = p.din<float>(ih); a.hist = p.din<float>(ihist); a.fin = p.din<bool>(ifin);
+  a.total = p.din<int>(itot); a.table = p.din<int>(itab);
+  a.t = p.din<int>(it); a.u = p.din<int>(iu);
+  a.input_length = p.din<int>(iil); a.output_length = p.din<int>(iol);
+  a.special_id = zero_duration_id; a.allow_skip = allow_skip; a.test_mode = test_mode;
+  a.prediction = p.dout<int>(op); a.log_prob = p.dout<float>(ol); a.next_t = p.dout<int>(ot);
+  a.next_u = p.dout<int>(ou); a.next_fin = p.dout<bool>(of); a.next_total = p.dout<int>(otd);
+  a.beam_branch = p.dout<int>(ob);
+  a.status = p.dstatus();
+  stage_out(p, launch_decode_step(a, g_ctx.stream), fn, true);
+}
+
+void ssnt_order_beam_branch(const int* final_branch, const int* beam_branch, int batch_size,
+                            int beam_width, int max_t, int* ordered_beam_branch) {
+  static const char* fn = "ssnt_order_beam_branch";
+  check_ptr(final_branch, fn, "final_branch"); check_ptr(beam_branch, fn, "beam_branch");
+  check_ptr(ordered_beam_branch, fn, "ordered_beam_branch");
+  if (batch_size < 0 || beam_width <= 0 || max_t <= 0)
+    fail(fn, "chunk size must be non-zero (beam_width / max_t <= 0)");
+  if (batch_size == 0) return;
+  ctx_ready(fn, true);
+  const size_t BW = (size_t)batch_size * beam_width;
+  Plan p;
+  const int ifb = p.add_in(final_branch, BW * 4), ib = p.add_in(beam_branch, BW * max_t * 4);
+  const int oo = p.add_out(ordered_beam_branch, BW * max_t * 4);
+  stage_in(p, fn, true);
+  const int rc = launch_order_beam_branch(batch_size, beam_width, max_t, p.din<int>(ifb),
+                                          p.din<int>(ib), p.dout<int>(oo), p.dstatus(),
+                                          g_ctx.stream);
+  stage_out(p, rc, fn, true);
+}
+
+void ssnt_upsample_source_indexes(const int* duration, const int* output_length, int batch_size,
+                                  int beam_width, int max_t, int max_u,
+                                  int* upsampled_source_indexes) {
+  static const char* fn = "ssnt_upsample_source_indexes";
+  check_ptr(duration, fn, "duration"); check_ptr(output_length, fn, "output_length");
+  check_ptr(upsampled_source_indexes, fn, "upsampled_source_indexes");
+  if (batch_size < 0 || beam_width <= 0 || max_t <= 0 || max_u <= 0)
+    fail(fn, "chunk size must be non-zero (beam_width / max_t / max_u <= 0)");
+  if (batch_size == 0) return;
+  ctx_ready(fn, true);
+  const size_t BW = (size_t)batch_size * beam_width;
+  Plan p;
+  const int id = p.add_in(duration, BW * max_t * 4), il = p.add_in(output_length, BW * 4);
+  // rows are written only up to output_length: upload the caller's prefill (the TF op fills
+  // out_of_range_source_index, upsample_source_indexes_op.cc:75) so it survives the download
+  const int oo = p.add_out(upsampled_source_indexes, BW * max_u * 4, upsampled_source_indexes);
+  stage_in(p, fn, true);
+  const int rc = launch_upsample(batch_size, beam_width, max_t, max_u, p.din<int>(id),
+                                 p.din<int>(il), p.dout<int>(oo), p.dstatus(), g_ctx.stream);
+  stage_out(p, rc, fn, true);
+}
+
+void tone_latent_beam_search_decode(const float* h, const float* log_prob_history,
+                                    const bool* is_finished, const int* t, const int* u,
+                                    const int* input_length, int batch_size, int beam_width,
+                                    int tone_class_size, int empty_tone_id, int* prediction,
+                                    float* log_probs, int* next_t, int* next_u,
+                                    bool* next_is_finished, int* beam_branch) {
+  static const char* fn = "tone_latent_beam_search_decode";
+  check_ptr(h, fn, "h"); check_ptr(log_prob_history, fn, "log_prob_history");
+  check_ptr(is_finished, fn, "is_finished"); check_ptr(t, fn, "t"); check_ptr(u, fn, "u");
+  check_ptr(input_length, fn, "input_length"); check_ptr(prediction, fn, "prediction");
+  check_ptr(log_probs, fn, "log_probs"); check_ptr(next_t, fn, "next_t");
+  check_ptr(next_u, fn, "next_u"); check_ptr(next_is_finished, fn, "next_is_finished");
+  check_ptr(beam_branch, fn, "beam_branch");
+  if (batch_size < 0 || beam_width <= 0 || tone_class_size <= 0)
+    fail(fn, "chunk size must be non-zero (beam_width / tone_class_size <= 0)");
+  if (batch_size == 0) return;
+  ctx_ready(fn, true);
+  const size_t BW = (size_t)batch_size * beam_width, C = tone_class_size;
+  Plan p;
+  const int ih = p.add_in(h, BW * C * 4), ihist = p.add_in(log_prob_history, BW * 4),
+            ifin = p.add_in(is_finished, BW), it = p.add_in(t, BW * 4), iu = p.add_in(u, BW * 4),
+            iil = p.add_in(input_length, (size_t)batch_size * 4);
+  const int op = p.add_out(prediction, BW * 4), ol = p.add_out(log_probs, BW * 4),
+            ot = p.add_out(next_t, BW * 4), ou = p.add_out(next_u, BW * 4),
+            of = p.add_out(next_is_finished, BW), ob = p.add_out(beam_branch, BW * 4);
+  stage_in(p, fn, true);
+  StepArgs a{};
+  a.variant = Variant::Tone;
+  a.B = batch_size; a.W = beam_width; a.Wmax = beam_width; a.C = tone_class_size;
+  a.h = p.din<float>(ih); a.hist = p.din<float>(ihist); a.fin = p.din<bool>(ifin);
+  a.t = p.din<int>(it); a.u = p.din<int>(iu); a.input_length = p.din<int>(iil);
+  a.special_id = empty_tone_id;
+  a.prediction = p.dout<int>(op); a.log_prob = p.dout<float>(ol); a.next_t = p.dout<int>(ot);
+  a.next_u = p.dout<int>(ou); a.next_fin = p.dout<bool>(of); a.beam_branch = p.dout<int>(ob);
+  a.status = p.dstatus();
+  stage_out(p, launch_decode_step(a, g_ctx.stream), fn, true);
+}
+
+void tone_latent_levenshtein_edit_distance(const int* a, const int* b, const int* a_lengths,
+                                           const int* b_lengths, int batch_size, int max_length,
+                                           int* distance) {
+  static const char* fn = "tone_latent_levenshtein_edit_distance";
+  check_ptr(a, fn, "a"); check_ptr(b, fn, "b"); check_ptr(a_lengths, fn, "a_lengths");
+  check_ptr(b_lengths, fn, "b_lengths"); check_ptr(distance, fn, "distance");
+  if (batch_size < 0 || max_length < 0) fail(fn, "invalid batch_size / max_length");
+  for (int i = 0; i < batch_size; ++i)  // `&a[..a_length]` slice bounds (src/edit_distance.rs:17-18)
+    if (a_lengths[i] < 0 || a_lengths[i] > max_length || b_lengths[i] < 0 || b_lengths[i] > max_length)
+      fail(fn, "range end index out of range for slice (length > max_length)");
+  if (batch_size == 0) return;
+  if (max_length == 0) {
+    for (int i = 0; i < batch_size; ++i) distance[i] = 0;
+    return;
+  }
+  ctx_ready(fn, true);
+  const size_t n = (size_t)batch_size * max_length;
+  Plan p;
+  const int ia = p.add_in(a, n * 4), ib = p.add_in(b, n * 4),
+            ial = p.add_in(a_lengths, (size_t)batch_size * 4),
+            ibl = p.add_in(b_lengths, (size_t)batch_size * 4);
+  const int od = p.add_out(distance, (size_t)batch_size * 4);
+  stage_in(p, fn, true);
+  const int rc = launch_levenshtein(batch_size, max_length, p.din<int>(ia), p.din<int>(ib),
+                                    p.din<int>(ial), p.din<int>(ibl), p.dout<int>(od),
+                                    g_ctx.stream);
+  stage_out(p, rc, fn, true);
+}
+
+// ------------------------------- extensions ---------------------------------------------------
+
+size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos) {
+  if (batch <= 0 || max_steps <= 0 || max_pos <= 0) return 0;
+  return fwd_bwd_workspace_bytes(batch, max_steps, max_pos);
+}
+
+int ssnt_fwd_bwd_device(const float* log_trans, const float* log_obs, const int* step_len,
+                        const int* pos_len, int batch, int max_steps, int max_pos, int flags,
+                        float* loss, float* grad_trans, float* grad_obs, float* log_alpha,
+                        float* log_beta, void* workspace, size_t workspace_bytes, int* status,
+                        void* stream) {
+  FwdBwdArgs a{};
+  a.log_trans = log_trans; a.log_obs = log_obs; a.step_len = step_len; a.pos_len = pos_len;
+  a.B = batch; a.T = max_steps; a.U = max_pos; a.flags = flags;
+  a.loss = loss; a.grad = grad_trans; a.grad_obs = grad_obs;
+  a.log_alpha = log_alpha; a.log_beta = log_beta;
+  a.workspace = workspace; a.workspace_bytes = workspace_bytes; a.status = status;
+  return launch_fwd_bwd(a, as_stream(stream));
+}
+
+int ssnt_fwd_bwd(const float* log_trans, const float* log_obs, const int* step_len,
+                 const int* pos_len, int batch, int max_steps, int max_pos, int flags,
+                 float* loss, float* grad_trans, float* grad_obs, float* log_alpha,
+                 float* log_beta) {
+  static const char* fn = "ssnt_fwd_bwd";
+  if (!log_trans || !step_len || !pos_len || !loss || batch < 0 || max_steps <= 0 || max_pos <= 0)
+    return SSNT_ERR_INVALID_ARG;
+  if (grad_obs && !log_obs) return SSNT_ERR_INVALID_ARG;
+  if (batch == 0) return SSNT_OK;
+  int rc = ctx_ready(fn, false);
+  if (rc != SSNT_OK) return rc;
+  const size_t cells = (size_t)batch * max_steps * max_pos;
+  const size_t ws = fwd_bwd_workspace_bytes(batch, max_steps, max_pos);
+  Plan p;
+  const int ilt = p.add_in(log_trans, cells * 8), isl = p.add_in(step_len, (size_t)batch * 4),
+            ipl = p.add_in(pos_len, (size_t)batch * 4);
+  const int ilo = log_obs ? p.add_in(log_obs, cells * 4) : -1;
+  const int ol = p.add_out(loss, (size_t)batch * 4);
+  const int og = grad_trans ? p.add_out(grad_trans, cells * 8) : -1;
+  const int ogo = grad_obs ? p.add_out(grad_obs, cells * 4) : -1;
+  const int ola = log_alpha ? p.add_out(log_alpha, cells * 4) : -1;
+  const int olb = log_beta ? p.add_out(log_beta, cells * 4) : -1;
+  rc = stage_in(p, fn, false, ws);  // the workspace is device-only, reserved after the plan
+  if (rc != SSNT_OK) return rc;
+  const size_t ws_off = Plan::align(p.total);
+  FwdBwdArgs a{};
+  a.log_trans = p.din<float>(ilt); a.log_obs = log_obs ? p.din<float>(ilo) : nullptr;
+  a.step_len = p.din<int>(isl); a.pos_len = p.din<int>(ipl);
+  a.B = batch; a.T = max_steps; a.U = max_pos; a.flags = flags;
+  a.loss = p.dout<float>(ol);
+  a.grad = og >= 0 ? p.dout<float>(og) : nullptr;
+  a.grad_obs = ogo >= 0 ? p.dout<float>(ogo) : nullptr;
+  a.log_alpha = ola >= 0 ? p.dout<float>(ola) : nullptr;
+  a.log_beta = olb >= 0 ? p.dout<float>(olb) : nullptr;
+  a.workspace = ws ? g_ctx.d + ws_off : nullptr;
+  a.workspace_bytes = ws;
+  a.status = p.dstatus();
+  return stage_out(p, launch_fwd_bwd(a, g_ctx.stream), fn, false);
+}
+
+int ssnt_beam_search_decode_device(const float* h, const float* log_prob_history,
+                                   const bool* is_finished, const int* t, const int* u,
+                                   const int* input_length, int batch_size, int beam_width,
+                                   int* prediction, float* log_probs, int* next_t, int* next_u,
+                                   bool* next_is_finished, int* beam_branch, int* status,
+                                   void* stream) {
+  if (!h || !log_prob_history || !is_finished || !t || !u || !input_length || !prediction ||
+      !log_probs || !next_t || !next_u || !next_is_finished || !beam_branch)
+    return SSNT_ERR_INVALID_ARG;
+  StepArgs a{};
+  a.variant = Variant::V1;
+  a.B = batch_size; a.W = beam_width; a.Wmax = beam_width; a.C = 2;
+  a.h = h; a.hist = log_prob_history; a.fin = is_finished; a.t = t; a.u = u;
+  a.input_length = input_length;
+  a.prediction = prediction; a.log_prob = log_probs; a.next_t = next_t; a.next_u = next_u;
+  a.next_fin = next_is_finished; a.beam_branch = beam_branch; a.status = status;
+  return launch_decode_step(a, as_stream(stream));
+}
+
+int ssnt_v2_beam_search_decode_device(const float* h, const float* log_prob_history,
+                                      const bool* is_finished, const int* total_duration,
+                                      const int* duration_table, const int* t, const int* u,
+                                      const int* input_length, const int* output_length,
+                                      int batch_size, int beam_width, int duration_class_size,
+                                      int zero_duration_id, bool allow_skip, bool test_mode,
+                                      int* prediction, float* log_probs, int* next_t,
+                                      int* next_u, bool* next_is_finished,
+                                      int* next_total_duration, int* beam_branch, int* status,
+                                      void* stream) {
+  if (!h || !log_prob_history || !is_finished || !total_duration || !duration_table || !t || !u ||
+      !input_length || !output_length || !prediction || !log_probs || !next_t || !next_u ||
+      !next_is_finished || !next_total_duration || !beam_branch)
+    return SSNT_ERR_INVALID_ARG;
+  StepArgs a{};
+  a.variant = Variant::V2;
+  a.B = batch_size; a.W = beam_width; a.Wmax = beam_width; a.C = duration_class_size;
+  a.h = h; a.hist = log_prob_history; a.fin = is_finished; a.total = total_duration;
+  a.table = duration_table; a.t = t; a.u = u;
+  a.input_length = input_length; a.output_length = output_length;
+  a.special_id = zero_duration_id; a.allow_skip = allow_skip; a.test_mode = test_mode;
+  a.prediction = prediction; a.log_prob = log_probs; a.next_t = next_t; a.next_u = next_u;
+  a.next_fin = next_is_finished; a.next_total = next_total_duration;
+  a.beam_branch = beam_branch; a.status = status;
+  return launch_decode_step(a, as_stream(stream));
+}
+
+int ssnt_tone_latent_beam_search_decode_device(const float* h, const float* log_prob_history,
+                                               const bool* is_finished, const int* t,
+                                               const int* u, const int* input_length,
+                                               int batch_size, int beam_width,
+                                               int tone_class_size, int empty_tone_id,
+                                               int* prediction, float* log_probs, int* next_t,
+                                               int* next_u, bool* next_is_finished,
+                                               int* beam_branch, int* status, void* stream) {
+  if (!h || !log_prob_history || !is_finished || !t || !u || !input_length || !prediction ||
+      !log_probs || !next_t || !next_u || !next_is_finished || !beam_branch)
+    return SSNT_ERR_INVALID_ARG;
+  StepArgs a{};
+  a.variant = Variant::Tone;
+  a.B = batch_size; a.W = beam_width; a.Wmax = beam_width; a.C = tone_class_size;
+  a.h = h; a.hist = log_prob_history; a.fin = is_finished; a.t = t; a.u = u;
+  a.input_length = input_length; a.special_id = empty_tone_id;
+  a.prediction = prediction; a.log_prob = log_probs; a.next_t = next_t; a.next_u = next_u;
+  a.next_fin = next_is_finished; a.beam_branch = beam_branch; a.status = status;
+  return launch_decode_step(a, as_stream(stream));
+}
+
+int ssnt_lattice_beam_search_decode_device(const float* lattice, const int* input_length,
+                                           int batch_size, int max_steps, int max_pos,
+                                           int beam_width, int* prediction, float* log_probs,
+                                           int* next_t, int* next_u, bool* next_is_finished,
+                                           int* beam_branch, int* best_beam_branch,
+                                           int* best_t_history, int* status, void* stream) {
+  if (!lattice || !input_length || !prediction || !log_probs || !next_t || !next_u ||
+      !next_is_finished || !beam_branch || !best_beam_branch || !best_t_history)
+    return SSNT_ERR_INVALID_ARG;
+  LatticeDecodeArgs a{};
+  a.B = batch_size; a.T = max_steps; a.U = max_pos; a.W = beam_width;
+  a.lattice = lattice; a.input_length = input_length;
+  a.prediction = prediction; a.log_prob = log_probs; a.next_t = next_t; a.next_u = next_u;
+  a.next_fin = next_is_finished; a.beam_branch = beam_branch;
+  a.best_beam_branch = best_beam_branch; a.best_t_history = best_t_history; a.status = status;
+  return launch_lattice_decode(a, as_stream(stream));
+}
+
+int ssnt_extract_best_beam_branch_device(const int* best_final_branch, const int* beam_branch,
+                                         const int* t_history, int batch_size, int beam_width,
+                                         int max_u, int* best_beam_branch, int* best_t_history,
+                                         int* status, void* stream) {
+  if (!beam_branch || !t_history || !best_beam_branch || !best_t_history)
+    return SSNT_ERR_INVALID_ARG;
+  return launch_extract_best(batch_size, beam_width, max_u, best_final_branch, beam_branch,
+                             t_history, best_beam_branch, best_t_history, status,
+                             as_stream(stream));
+}
+
+int ssnt_order_beam_branch_device(const int* final_branch, const int* beam_branch,
+                                  int batch_size, int beam_width, int max_t,
+                                  int* ordered_beam_branch, int* status, void* stream) {
+  if (!final_branch || !beam_branch || !ordered_beam_branch) return SSNT_ERR_INVALID_ARG;
+  return launch_order_beam_branch(batch_size, beam_width, max_t, final_branch, beam_branch,
+                                  ordered_beam_branch, status, as_stream(stream));
+}
+
+int ssnt_upsample_source_indexes_device(const int* duration, const int* output_length,
+                                        int batch_size, int beam_width, int max_t, int max_u,
+                                        int* upsampled_source_indexes, int* status,
+                                        void* stream) {
+  if (!duration || !output_length || !upsampled_source_indexes) return SSNT_ERR_INVALID_ARG;
+  return launch_upsample(batch_size, beam_width, max_t, max_u, duration, output_length,
+                         upsampled_source_indexes, status, as_stream(stream));
+}
+
+int ssnt_levenshtein_edit_distance_device(const int* a, const int* b, const int* a_lengths,
+                                          const int* b_lengths, int batch_size, int max_length,
+                                          int* distance, void* stream) {
+  if (!a || !b || !a_lengths || !b_lengths || !distance) return SSNT_ERR_INVALID_ARG;
+  return launch_levenshtein(batch_size, max_length, a, b, a_lengths, b_lengths, distance,
+                            as_stream(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,524 @@
+// decode.hip -- beam-search decode steps and alignment utilities for gfx950.
+//
+// One wave (64 lanes) owns one batch element. A step generates every candidate of every beam
+// into LDS, ranks them (stable descending sort on log_prob, generation index as tie-break,
+// src/lib.rs:161), drops consecutive duplicates (src/lib.rs:162), optionally injects v2's
+// on-diagonal candidate (src/v2.rs:283-308) and pads cyclically (src/lib.rs:163-167). All of it
+// is integer / compare work plus one f32 add per candidate, so the result is bit-exact with the
+// Rust step (and with oracle/ssnt_oracle.c) by construction.
+#include <hip/hip_runtime.h>
+
+#include "ssnt_internal.h"
+
+namespace ssnt {
+namespace {
+
+typedef unsigned long long u64;
+
+struct Cand {
+  u64 nt, nu;  // next_t / next_u as Rust usize
+  float lp;
+  int pred, parent, tot;
+  int fin, valid;
+};
+
+__device__ __forceinline__ u64 as_usize(int v) { return (u64)(long long)v; }
+
+// Rust `f32 as i32` (saturating, NaN -> 0)
+__device__ __forceinline__ int f2i_sat(float x) {
+  if (x != x) return 0;
+  if (x >= 2147483648.0f) return 2147483647;
+  if (x <= -2147483648.0f) return (-2147483647 - 1);
+  return (int)x;
+}
+
+__device__ __forceinline__ bool cand_eq(const Cand& a, const Cand& b, bool with_tot) {
+  return a.pred == b.pred && a.lp == b.lp && a.nt == b.nt && a.nu == b.nu && a.fin == b.fin &&
+         (!with_tot || a.tot == b.tot);
+}
+
+struct BatchView {
+  const float* h;
+  const float* hist;
+  const bool* fin;
+  const int* t;
+  const int* u;
+  const int* total;
+  u64 I, O;
+};
+
+// Candidate c = w*C + i (generation order of src/lib.rs:150-158's ordered flat_map).
+__device__ Cand gen_candidate(const StepArgs& a, const BatchView& v, int c) {
+  const int C = a.C;
+  const int w = c / C, i = c - w * C;
+  const u64 t = as_usize(v.t[w]);
+  const u64 u = as_usize(v.u[w]);
+  const float hist = v.hist[w];
+  const bool defined = (t < v.I) && !v.fin[w];  // decode_beam_at (src/lib.rs:57-67 etc.)
+  Cand r;
+  r.parent = w;
+  r.tot = 0;
+  if (!defined) {  // "End of input. Return values to fill padding region."
+    r.valid = (i == 0);
+    r.pred = a.variant == Variant::V1 ? 0 : a.special_id;
+    r.lp = hist;
+    r.nt = t;
+    r.nu = u;
+    r.fin = 1;
+    r.tot = a.variant == Variant::V2 ? v.total[w] : 0;
+    return r;
+  }
+  const float hv = v.h[w * C + i];
+  r.valid = 1;
+  if (a.variant == Variant::V1) {  // src/lib.rs:186-227
+    const u64 last = v.I - 1;
+    if (i == 0 && t == last) {
+      r.pred = 0; r.lp = hist + hv; r.nt = t; r.nu = u; r.fin = 1;
+    } else if (i == 1 && t == last) {  // prohibited shift
+      r.pred = 0; r.lp = hist; r.nt = t; r.nu = u; r.fin = 1;
+    } else if (i == 1) {
+      r.pred = 1; r.lp = hist + hv; r.nt = t + 1; r.nu = u + 1; r.fin = 0;
+    } else {
+      r.pred = 0; r.lp = hist + hv; r.nt = t; r.nu = u + 1; r.fin = 0;
+    }
+    return r;
+  }
+  if (a.variant == Variant::Tone) {  // src/tone_latent.rs:426-433, 560-570
+    r.pred = i; r.lp = hist + hv; r.nt = t + 1; r.nu = u + 1; r.fin = 0;
+    return r;
+  }
+  // v2: src/v2.rs:119-166, 326-336
+  const int duration = a.table[i];
+  const int tot = (int)((unsigned)v.total[w] + (unsigned)duration);
+  const float diagonal = (float)v.O / (float)v.I * (float)(t + 1);
+  const float upper_range = (float)v.O * 0.1f;
+  const float lower_range = (float)v.O * 0.05f;
+  const int lb = f2i_sat(fmaxf(diagonal - lower_range, 0.0f));
+  const int ub = f2i_sat(fminf(diagonal + upper_range, (float)v.O));
+  const u64 remaining = v.I - (t + 1);
+  const bool overrun = remaining * 3 > v.O;
+  bool fin = false;
+  bool ok = true;
+  if (!a.test_mode && (tot < lb || tot > ub)) ok = false;
+  else if (!a.test_mode && overrun) ok = false;
+  else if (t == v.I - 1) {
+    if (!a.test_mode && tot != (int)v.O) ok = false;
+    else if (!a.allow_skip && i == a.special_id) ok = false;
+    else fin = true;
+  } else if (!a.allow_skip && i == a.special_id) ok = false;
+  r.valid = ok;
+  r.pred = i;
+  r.lp = hist + hv;
+  r.nt = fin ? t : t + 1;
+  r.nu = fin ? u : u + 1;
+  r.fin = fin;
+  r.tot = tot;
+  return r;
+}
+
+__device__ __forceinline__ bool on_diagonal(const BatchView& v, const Cand& r) {
+  const float diagonal = (float)v.O / (float)v.I * (float)r.nt;  // src/v2.rs:113-117
+  const float diff = (float)r.tot - diagonal;
+  return diff >= -20.0f && diff <= 0.0f;
+}
+
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  return x;
+}
+__device__ __forceinline__ int wave_min(int x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x = min(x, __shfl_xor(x, off));
+  return x;
+}
+
+// One decode step for one batch element, executed by the whole wave. `cand` has n = W*C
+// entries, `order` and `kept` n ints each (LDS). Writes the Wmax result slots through `emit`.
+// Returns n_kept (0 = no candidate).
+template <typename Emit>
+__device__ int step_wave(const StepArgs& a, const BatchView& v, Cand* cand, int* order, int* kept,
+                         int Wmax, Emit emit) {
+  const int lane = threadIdx.x & 63;
+  const int n = a.W * a.C;
+  for (int c = lane; c < n; c += 64) cand[c] = gen_candidate(a, v, c);
+  __syncthreads();
+  // rank = position in the stable descending sort
+  int nvalid_local = 0;
+  for (int c = lane; c < n; c += 64) {
+    const Cand me = cand[c];
+    if (!me.valid) continue;
+    ++nvalid_local;
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+      const float lj = cand[j].lp;
+      const int vj = cand[j].valid;
+      rank += (vj && (lj > me.lp || (lj == me.lp && j < c))) ? 1 : 0;
+    }
+    order[rank] = c;
+  }
+  const int nvalid = wave_sum(nvalid_local);
+  __syncthreads();
+  // consecutive dedup (keep first of each run), stream-compacted into kept[]
+  const bool with_tot = a.variant == Variant::V2;
+  int base = 0;
+  for (int r0 = 0; r0 < nvalid; r0 += 64) {
+    const int r = r0 + lane;
+    bool keep = false;
+    if (r < nvalid) keep = (r == 0) || !cand_eq(cand[order[r]], cand[order[r - 1]], with_tot);
+    const u64 mask = __ballot(keep);
+    const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+    if (keep) kept[pos] = order[r];
+    base += __popcll(mask);
+  }
+  const int nkept = base;
+  __syncthreads();
+  if (nkept == 0) return 0;
+  int diag = nkept;  // first kept candidate on the diagonal (v2, not test_mode)
+  if (a.variant == Variant::V2 && !a.test_mode) {
+    int best = nkept;
+    for (int k = lane; k < nkept; k += 64)
+      if (on_diagonal(v, cand[kept[k]])) {
+        best = k;
+        break;
+      }
+    diag = wave_min(best);
+  }
+  for (int i = lane; i < Wmax; i += 64) {
+    const int k = (diag < nkept && i == Wmax - 1) ? diag : (i % nkept);
+    emit(i, cand[kept[k]]);
+  }
+  return nkept;
+}
+
+__global__ __launch_bounds__(64) void k_decode_step(StepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int n = a.W * a.C;
+  Cand* cand = reinterpret_cast<Cand*>(smem);
+  int* order = reinterpret_cast<int*>(cand + n);
+  int* kept = order + n;
+  BatchView v;
+  const size_t bw = (size_t)b * a.W;
+  v.h = a.h + bw * a.C;
+  v.hist = a.hist + bw;
+  v.fin = a.fin + bw;
+  v.t = a.t + bw;
+  v.u = a.u + bw;
+  v.total = a.total ? a.total + bw : nullptr;
+  v.I = as_usize(a.input_length ? a.input_length[b] : a.scalar_input_length);
+  v.O = as_usize(a.output_length ? a.output_length[b] : 0);
+  const size_t o = (size_t)b * a.Wmax;
+  const int nk = step_wave(a, v, cand, order, kept, a.Wmax, [&](int i, const Cand& r) {
+    a.prediction[o + i] = r.pred;  // src/lib.rs:138-145
+    a.log_prob[o + i] = r.lp;
+    a.next_t[o + i] = (int)(unsigned)r.nt;
+    a.next_u[o + i] = (int)(unsigned)r.nu;
+    a.beam_branch[o + i] = r.parent;
+    a.next_fin[o + i] = r.fin != 0;
+    if (a.next_total) a.next_total[o + i] = r.tot;
+  });
+  if (nk == 0 && a.status && (threadIdx.x & 63) == 0) atomicOr(a.status, kStatusNoCandidate);
+}
+
+// Fused multi-step v1 decode: the whole T-step loop of one utterance in one wave. Beam state
+// lives in lanes 0..W-1; step s reads h[w] = lattice[b, u_w, t_w, :] (row s staged in LDS).
+__global__ __launch_bounds__(64) void k_lattice_decode(LatticeDecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int W = a.W, T = a.T, U = a.U;
+  const int n = 2 * W;
+  Cand* cand = reinterpret_cast<Cand*>(smem);
+  int* order = reinterpret_cast<int*>(cand + n);
+  int* kept = order + n;
+  float* hbuf = reinterpret_cast<float*>(kept + n);   // (W,2)
+  float* hist = hbuf + 2 * W;                         // (W)
+  int* tt = reinterpret_cast<int*>(hist + W);         // (W)
+  int* uu = tt + W;                                   // (W)
+  bool* ff = reinterpret_cast<bool*>(uu + W);         // (W)
+  StepArgs sa{};
+  sa.variant = Variant::V1;
+  sa.B = a.B;
+  sa.W = W;
+  sa.Wmax = W;
+  sa.C = 2;
+  BatchView v;
+  v.h = hbuf;
+  v.hist = hist;
+  v.fin = ff;
+  v.t = tt;
+  v.u = uu;
+  v.total = nullptr;
+  v.I = as_usize(a.input_length[b]);
+  v.O = 0;
+  const float* lat = a.lattice + (size_t)b * T * U * 2;
+  for (int w = lane; w < W; w += 64) {
+    hist[w] = 0.0f;
+    tt[w] = 0;
+    uu[w] = 0;
+    ff[w] = false;
+  }
+  __syncthreads();
+  for (int s = 0; s < T; ++s) {
+    for (int w = lane; w < W; w += 64) {
+      const bool defined = !ff[w] && as_usize(tt[w]) < v.I && (unsigned)uu[w] < (unsigned)T &&
+                           (unsigned)tt[w] < (unsigned)U;
+      const float2 x = defined ? *reinterpret_cast<const float2*>(lat + ((size_t)uu[w] * U + tt[w]) * 2)
+                               : make_float2(0.0f, 0.0f);
+      hbuf[2 * w] = x.x;
+      hbuf[2 * w + 1] = x.y;
+    }
+    __syncthreads();
+    const size_t o = ((size_t)b * T + s) * W;
+    // results are staged in registers, state is updated after every lane has read it
+    int rnt = 0, rnu = 0;
+    float rlp = 0.0f;
+    bool rfin = false;
+    step_wave(sa, v, cand, order, kept, W, [&](int i, const Cand& r) {
+      a.prediction[o + i] = r.pred;
+      a.log_prob[o + i] = r.lp;
+      a.next_t[o + i] = (int)(unsigned)r.nt;
+      a.next_u[o + i] = (int)(unsigned)r.nu;
+      a.beam_branch[o + i] = r.parent;
+      a.next_fin[o + i] = r.fin != 0;
+      rlp = r.lp;
+      rnt = (int)(unsigned)r.nt;
+      rnu = (int)(unsigned)r.nu;
+      rfin = r.fin != 0;
+    });
+    __syncthreads();
+    if (lane < W) {
+      hist[lane] = rlp;
+      tt[lane] = rnt;
+      uu[lane] = rnu;
+      ff[lane] = rfin;
+    }
+    __syncthreads();
+  }
+}
+
+// Backtrace along beam_branch (B,T,W) for n_paths (<= 64) final branches per batch element
+// (util.rs:20-33 with n_paths = 1 and t history; v2_util.rs:6-36 with n_paths = W). A null
+// final_branch means branch 0 (the best slot after the final sort). Rows are staged into LDS
+// in chunks (coalesced), then lane k walks path k back through the chunk.
+__global__ __launch_bounds__(64) void k_backtrace(int B, int W, int T, int n_paths,
+                                                  const int* __restrict__ final_branch,
+                                                  const int* __restrict__ beam_branch,
+                                                  const int* __restrict__ t_history,
+                                                  int* __restrict__ out_branch,
+                                                  int* __restrict__ out_t, int chunk, int* status) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int* sb = reinterpret_cast<int*>(smem);
+  int* st = sb + (size_t)chunk * W;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int* bb = beam_branch + (size_t)b * T * W;
+  const int* th = t_history ? t_history + (size_t)b * T * W : nullptr;
+  const bool active = lane < n_paths;
+  int c = (active && final_branch) ? final_branch[(size_t)b * n_paths + lane] : 0;
+  int* ob = out_branch + ((size_t)b * n_paths + lane) * T;
+  int* ot = out_t ? out_t + ((size_t)b * n_paths + lane) * T : nullptr;
+  bool bad = false;
+  for (int hi = T; hi > 0; hi -= chunk) {
+    const int lo = max(hi - chunk, 0);
+    const int cnt = (hi - lo) * W;
+    __syncthreads();
+    for (int i = lane; i < cnt; i += 64) {
+      sb[i] = bb[(size_t)lo * W + i];
+      if (th) st[i] = th[(size_t)lo * W + i];
+    }
+    __syncthreads();
+    if (active) {
+      for (int s = hi - 1; s >= lo; --s) {
+        if (c < 0 || c >= W) {  // Rust would panic on the out-of-bounds index
+          bad = true;
+          c = c < 0 ? 0 : W - 1;
+        }
+        ob[s] = c;
+        const int r = (s - lo) * W + c;
+        if (ot) ot[s] = st[r];
+        c = sb[r];
+      }
+    }
+  }
+  if (bad && status) atomicOr(status, kStatusBadIndex);
+}
+
+__device__ __forceinline__ int wave_incl_scan_add(int x, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ int wave_incl_scan_min(int x, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x = min(x, y);
+  }
+  return x;
+}
+
+// upsample_source_indexes (src/v2_util.rs:39-66): one wave per (b,w) row.
+__global__ __launch_bounds__(64) void k_upsample(int rows, int T, int max_u,
+                                                 const int* __restrict__ duration,
+                                                 const int* __restrict__ output_length,
+                                                 int* __restrict__ out, int* status) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int* cum = reinterpret_cast<int*>(smem);  // inclusive prefix sums (T)
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int* d = duration + (size_t)r * T;
+  long long carry = 0;
+  bool neg = false;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + lane;
+    const int x = t < T ? d[t] : 0;
+    neg |= x < 0;
+    const int inc = wave_incl_scan_add(x, lane);
+    if (t < T) cum[t] = (int)(carry + inc);
+    carry += __shfl(inc, 63);
+  }
+  const bool anyneg = __any(neg);
+  const int L = output_length[r];
+  if (anyneg || carry != (long long)L) {
+    if (lane == 0 && status) atomicOr(status, kStatusDurationMismatch);
+    return;
+  }
+  __syncthreads();
+  const int n = min(L, max_u);
+  int* o = out + (size_t)r * max_u;
+  for (int k = lane; k < n; k += 64) {
+    int lo = 0, hi = T;  // first t with cum[t] > k
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cum[mid] > k) hi = mid;
+      else lo = mid + 1;
+    }
+    o[k] = lo;
+  }
+}
+
+// Levenshtein distance (src/edit_distance.rs:27-60, Kaldi): one wave per pair. Row m of the DP
+// is new[n] = n + prefix_min_{n'<=n}(base[n'] - n'), base[n] = min(e[n-1]+delta, e[n]+1),
+// base[0] = e[0]+1 -- the in-row dependency of the reference loop as a wave min-scan.
+__global__ __launch_bounds__(64) void k_levenshtein(int B, int L, const int* __restrict__ a,
+                                                    const int* __restrict__ bsq,
+                                                    const int* __restrict__ a_len,
+                                                    const int* __restrict__ b_len,
+                                                    int* __restrict__ dist) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int* e = reinterpret_cast<int*>(smem);  // (L+1)
+  int* nb = e + (L + 1);                  // (L+1)
+  const int i = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  // lengths outside [0, L] panic in the reference (slice bounds); the host layer rejects them,
+  // the kernel clamps so a bad device-side length can never read out of bounds
+  const int M = min(max(a_len[i], 0), L), N = min(max(b_len[i], 0), L);
+  const int* A = a + (size_t)i * L;
+  const int* Bv = bsq + (size_t)i * L;
+  for (int n = lane; n <= N; n += 64) e[n] = n;
+  __syncthreads();
+  for (int m = 1; m <= M; ++m) {
+    const int am = A[m - 1];
+    int carry = 0x3fffffff;
+    for (int n0 = 0; n0 <= N; n0 += 64) {
+      const int n = n0 + lane;
+      int base = 0x3fffffff;
+      if (n == 0) base = e[0] + 1;
+      else if (n <= N) base = min(e[n - 1] + (am == Bv[n - 1] ? 0 : 1), e[n] + 1);
+      int v = (n <= N) ? base - n : 0x3fffffff;
+      v = wave_incl_scan_min(v, lane);
+      v = min(v, carry);
+      if (n <= N) nb[n] = n + v;
+      carry = __shfl(v, 63);
+    }
+    __syncthreads();
+    for (int n = lane; n <= N; n += 64) e[n] = nb[n];
+    __syncthreads();
+  }
+  if (lane == 0) dist[i] = e[N];
+}
+
+inline int last_error() { return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP; }
+
+}  // namespace
+
+int launch_decode_step(const StepArgs& a, hipStream_t st) {
+  if (a.B < 0 || a.W <= 0 || a.Wmax <= 0 || a.C <= 0) return SSNT_ERR_INVALID_ARG;
+  if (a.variant == Variant::V1 && a.C != 2) return SSNT_ERR_INVALID_ARG;
+  if (a.variant == Variant::V2 && (!a.total || !a.table || !a.output_length || !a.next_total))
+    return SSNT_ERR_INVALID_ARG;
+  if (a.B == 0) return SSNT_OK;
+  const size_t n = (size_t)a.W * a.C;
+  const size_t lds = n * sizeof(Cand) + 2 * n * sizeof(int);
+  if (lds > 150 * 1024) return SSNT_ERR_UNSUPPORTED;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_decode_step),
+                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  hipLaunchKernelGGL(k_decode_step, dim3(a.B), dim3(64), lds, st, a);
+  return last_error();
+}
+
+int launch_lattice_decode(const LatticeDecodeArgs& a, hipStream_t st) {
+  if (a.B < 0 || a.W <= 0 || a.W > 64 || a.T <= 0 || a.U <= 0) return SSNT_ERR_INVALID_ARG;
+  if (a.B == 0) return SSNT_OK;
+  const size_t n = 2 * (size_t)a.W;
+  const size_t lds = n * sizeof(Cand) + 2 * n * sizeof(int) + (size_t)a.W * (2 + 1 + 1 + 1) * 4 + a.W + 16;
+  hipLaunchKernelGGL(k_lattice_decode, dim3(a.B), dim3(64), lds, st, a);
+  int rc = last_error();
+  if (rc != SSNT_OK) return rc;
+  // alignment of the best final beam (slot 0), t history = next_t (util.rs:20-33)
+  return launch_extract_best(a.B, a.W, a.T, nullptr, a.beam_branch, a.next_t, a.best_beam_branch,
+                             a.best_t_history, a.status, st);
+}
+
+int launch_extract_best(int B, int W, int U, const int* best_final_branch, const int* beam_branch,
+                        const int* t_history, int* best_beam_branch, int* best_t_history,
+                        int* status, hipStream_t st) {
+  if (B < 0 || W <= 0 || U < 0) return SSNT_ERR_INVALID_ARG;
+  if (B == 0 || U == 0) return SSNT_OK;
+  const int chunk = max(1, min(U, 8192 / W));
+  const size_t lds = (size_t)chunk * W * 2 * sizeof(int);
+  hipLaunchKernelGGL(k_backtrace, dim3(B), dim3(64), lds, st, B, W, U, 1, best_final_branch,
+                     beam_branch, t_history, best_beam_branch, best_t_history, chunk, status);
+  return last_error();
+}
+
+int launch_order_beam_branch(int B, int W, int T, const int* final_branch, const int* beam_branch,
+                             int* ordered, int* status, hipStream_t st) {
+  if (B < 0 || W <= 0 || T < 0) return SSNT_ERR_INVALID_ARG;
+  if (W > 64) return SSNT_ERR_UNSUPPORTED;
+  if (B == 0 || T == 0) return SSNT_OK;
+  const int chunk = max(1, min(T, 8192 / W));
+  const size_t lds = (size_t)chunk * W * 2 * sizeof(int);
+  hipLaunchKernelGGL(k_backtrace, dim3(B), dim3(64), lds, st, B, W, T, W, final_branch,
+                     beam_branch, nullptr, ordered, nullptr, chunk, status);
+  return last_error();
+}
+
+int launch_upsample(int B, int W, int T, int max_u, const int* duration, const int* output_length,
+                    int* out, int* status, hipStream_t st) {
+  if (B < 0 || W <= 0 || T < 0 || max_u < 0) return SSNT_ERR_INVALID_ARG;
+  if (B == 0) return SSNT_OK;
+  const size_t lds = (size_t)(T + 1) * sizeof(int);
+  if (lds > 150 * 1024) return SSNT_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_upsample, dim3(B * W), dim3(64), lds, st, B * W, T, max_u, duration,
+                     output_length, out, status);
+  return last_error();
+}
+
+int launch_levenshtein(int B, int max_length, const int* a, const int* b, const int* a_len,
+                       const int* b_len, int* dist, hipStream_t st) {
+  if (B < 0 || max_length < 0) return SSNT_ERR_INVALID_ARG;
+  if (B == 0) return SSNT_OK;
+  const size_t lds = (size_t)(max_length + 1) * 2 * sizeof(int);
+  if (lds > 150 * 1024) return SSNT_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_levenshtein, dim3(B), dim3(64), lds, st, B, max_length, a, b, a_len,
+                     b_len, dist);
+  return last_error();
+}
+
+}  // namespace ssnt

@@ -1,0 +1,95 @@
+// ssnt_internal.h -- launchers shared between the kernels (fwd_bwd.hip, decode.hip) and the
+// C-ABI host layer (capi.hip). Not part of the public interface (that is include/ssnt_tts_c.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ssnt_tts_c.h"
+
+namespace ssnt {
+
+// device status word bits (OR-ed by kernels, read by the host layer)
+constexpr int kStatusNoCandidate = 1 << 0;       // v2: no duration sequence fits (src/v2.rs:292)
+constexpr int kStatusDurationMismatch = 1 << 1;  // upsample: sum(d) != output_length (src/v2_util.rs:58)
+constexpr int kStatusBadLength = 1 << 2;         // fwd-bwd: step/pos length outside the tensor
+constexpr int kStatusBadIndex = 1 << 3;          // backtrace: branch index outside [0, W)
+
+int status_bits_to_code(int bits);
+
+// ---- lattice forward-backward (fwd_bwd.hip) ----
+struct FwdBwdArgs {
+  const float* log_trans;  // (B,T,U,2)
+  const float* log_obs;    // (B,T,U) or null
+  const int* step_len;     // (B)
+  const int* pos_len;      // (B)
+  int B, T, U, flags;
+  float* loss;       // (B)
+  float* grad;       // (B,T,U,2) or null
+  float* grad_obs;   // (B,T,U) or null (requires log_obs)
+  float* log_alpha;  // (B,T,U) or null
+  float* log_beta;   // (B,T,U) or null
+  void* workspace;   // row storage when the rows do not fit LDS
+  size_t workspace_bytes;
+  int* status;  // device status word or null
+};
+size_t fwd_bwd_workspace_bytes(int B, int T, int U);
+int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
+
+// ---- beam-search decode (decode.hip) ----
+enum class Variant : int { V1 = 0, V2 = 1, Tone = 2 };
+
+struct StepArgs {
+  Variant variant;
+  int B, W, Wmax, C;  // C: classes per beam (2 for v1, D for v2, tone classes)
+  const float* h;     // (B,W,C)
+  const float* hist;  // (B,W)
+  const bool* fin;    // (B,W)
+  const int* t;       // (B,W)
+  const int* u;       // (B,W)
+  const int* input_length;   // (B) (v1: may be null -> scalar_input_length)
+  int scalar_input_length;   // v1 reference symbol: one max_t for the batch (src/lib.rs:99)
+  const int* output_length;  // (B) v2
+  const int* total;          // (B,W) v2
+  const int* table;          // (D) v2
+  int special_id;            // v2 zero_duration_id / tone empty_tone_id
+  bool allow_skip, test_mode;
+  int* prediction;
+  float* log_prob;
+  int* next_t;
+  int* next_u;
+  bool* next_fin;
+  int* next_total;  // v2
+  int* beam_branch;
+  int* status;
+};
+int launch_decode_step(const StepArgs& a, hipStream_t stream);
+
+struct LatticeDecodeArgs {
+  int B, T, U, W;
+  const float* lattice;      // (B,T,U,2)
+  const int* input_length;   // (B)
+  int* prediction;           // (B,T,W)
+  float* log_prob;           // (B,T,W)
+  int* next_t;               // (B,T,W)
+  int* next_u;               // (B,T,W)
+  bool* next_fin;            // (B,T,W)
+  int* beam_branch;          // (B,T,W)
+  int* best_beam_branch;     // (B,T)
+  int* best_t_history;       // (B,T)
+  int* status;
+};
+int launch_lattice_decode(const LatticeDecodeArgs& a, hipStream_t stream);
+
+int launch_extract_best(int B, int W, int U, const int* best_final_branch, const int* beam_branch,
+                        const int* t_history, int* best_beam_branch, int* best_t_history,
+                        int* status, hipStream_t stream);
+int launch_order_beam_branch(int B, int W, int T, const int* final_branch,
+                             const int* beam_branch, int* ordered, int* status,
+                             hipStream_t stream);
+int launch_upsample(int B, int W, int T, int max_u, const int* duration,
+                    const int* output_length, int* out, int* status, hipStream_t stream);
+int launch_levenshtein(int B, int max_length, const int* a, const int* b, const int* a_len,
+                       const int* b_len, int* dist, hipStream_t stream);
+
+}  // namespace ssnt

@@ -1,0 +1,41 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+for p in (ROOT, ROOT / "ssnt-tts-rust_amd", ROOT / "oracle", ROOT / "tests"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+GOLDEN = ROOT / "tests" / "golden"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libssnt_tts_c.so)")
+    config.addinivalue_line("markers", "slow: long-running case")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle as O
+    O.lib()  # raises with a build hint if missing
+    return O
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no GPU is visible")
+    import ssnt_tts_amd
+    ssnt_tts_amd.load(require_gpu=True)
+    return ssnt_tts_amd
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    with open(GOLDEN / "reference_fixtures.json") as f:
+        return json.load(f)

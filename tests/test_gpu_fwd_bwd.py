@@ -1,0 +1,143 @@
+"""GPU parity for the lattice forward-backward (through libssnt_tts_c.so).
+
+Bar: BIT-EXACT against the split-exponent C oracle (oracle/ssnt_oracle.c) on loss, gradients,
+obs gradients and log-alpha / log-beta -- which itself is pinned to float64 truth within the
+north_star tolerance (tests/test_oracle_fwd_bwd.py: 1e-5 abs on gradients, 1e-5 + 2^-23|x| on
+log values). At full BASELINE sizes the same bit-exact check runs (the multi-threaded oracle
+finishes in seconds), plus size-independent properties (posterior mass 1 per step).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+F_TERM, F_ZINF = 1, 2
+
+
+def _run_gpu(gpu, lt, S, P, lo=None, flags=F_TERM, debug=True):
+    dev = torch.device("cuda:0")
+    r = gpu.ssnt_fwd_bwd(torch.from_numpy(lt).to(dev), torch.tensor(S, dtype=torch.int32, device=dev),
+                         torch.tensor(P, dtype=torch.int32, device=dev),
+                         None if lo is None else torch.from_numpy(lo).to(dev),
+                         terminal_emit=bool(flags & F_TERM), zero_infinity=bool(flags & F_ZINF),
+                         debug=debug, check=True)
+    return {k: v.cpu().numpy() for k, v in r.items() if k != "status"}
+
+
+def _assert_bit_exact(g, o, keys):
+    for k in keys:
+        a, b = g[k], o[k]
+        assert a.shape == b.shape, k
+        same = (a == b) | (np.isnan(a) & np.isnan(b))
+        if not np.all(same):
+            idx = np.argwhere(~same)[:5]
+            raise AssertionError(f"{k}: {np.sum(~same)} cells differ, e.g. {idx.tolist()} "
+                                 f"gpu={a[tuple(idx[0])]} oracle={b[tuple(idx[0])]}")
+
+
+SHAPES = [  # (B, T, U) -- covers K = 1, 2, 4, 8 lanes-per-position layouts and odd U
+    (1, 50, 20),    # BASELINE configs[0]
+    (3, 37, 64),    # K=1 upper edge
+    (4, 60, 65),    # K=2, odd U
+    (5, 90, 80),    # K=2, the config-2 position count
+    (3, 45, 130),   # K=4
+    (2, 30, 300),   # K=8
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("obs", [False, True])
+def test_bit_exact_full_lengths(gpu, oracle, shape, obs):
+    B, T, U = shape
+    lt = oracle.synth_log_trans(B, T, U, seed=B * 1000 + T)
+    lo = (np.random.default_rng(T).standard_normal((B, T, U)) * 15 - 40).astype(np.float32) if obs else None
+    S, P = [T] * B, [U] * B
+    if T < U:
+        P = [T] * B
+    g = _run_gpu(gpu, lt, S, P, lo)
+    o = oracle.fwd_bwd_xf(lt, S, P, log_obs=lo, debug=True)
+    keys = ["loss", "grad", "log_alpha", "log_beta"] + (["grad_obs"] if obs else [])
+    _assert_bit_exact(g, o, keys)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("flags", [F_TERM, 0, F_TERM | F_ZINF])
+def test_bit_exact_ragged_and_edges(gpu, oracle, seed, flags):
+    rng = np.random.default_rng(seed)
+    B, T, U = 9, 48, 33
+    P = rng.integers(1, U + 1, size=B)
+    S = np.array([rng.integers(max(1, p), T + 1) for p in P])
+    S[0], P[0] = 1, 1          # single cell
+    S[1], P[1] = 10, 12        # infeasible (S < P)
+    S[2], P[2] = 0, 1          # empty
+    S[3], P[3] = T, U          # full
+    S[4], P[4] = 20, 20        # S == P: one path
+    lt = oracle.synth_log_trans(B, T, U, seed=seed)
+    lt[5, :, 3, 1] = -np.inf   # log(0) transitions
+    lt[6, 10:30, :, 0] = -np.inf
+    g = _run_gpu(gpu, lt, S, P, flags=flags)
+    o = oracle.fwd_bwd_xf(lt, S, P, flags=flags, debug=True)
+    _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+
+
+def test_workspace_mode_long_rows(gpu, oracle):
+    # T*U*8 bytes > LDS budget -> rows live in the global workspace
+    B, T, U = 3, 320, 80
+    lt = oracle.synth_log_trans(B, T, U, seed=9)
+    S, P = [320, 250, 200], [80, 70, 33]
+    g = _run_gpu(gpu, lt, S, P)
+    o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
+    _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+
+
+def test_config2_full_size_bit_exact(gpu, oracle):
+    # BASELINE configs[1]: B=256 T=200 U=80, f32 loss + grad
+    B, T, U = 256, 200, 80
+    lt = oracle.synth_log_trans(B, T, U, seed=0)
+    S, P = [T] * B, [U] * B
+    g = _run_gpu(gpu, lt, S, P, debug=False)
+    o = oracle.fwd_bwd_xf(lt, S, P)
+    _assert_bit_exact(g, o, ["loss", "grad"])
+    occ = -g["grad"][:, :T - 1].sum(axis=(2, 3))  # posterior mass per transition step
+    assert np.max(np.abs(occ - 1.0)) < 1e-4
+
+
+def test_config5_long_form_properties(gpu, oracle):
+    # BASELINE configs[4] fwd-bwd: B=64 T=2000 U=400. Bit-exact on a sample of utterances,
+    # posterior-mass property on all of them.
+    B, T, U = 64, 2000, 400
+    lt = oracle.synth_log_trans(B, T, U, seed=4)
+    S, P = [T] * B, [U] * B
+    g = _run_gpu(gpu, lt, S, P, debug=False)
+    occ = -g["grad"][:, :T - 1].sum(axis=(2, 3))
+    assert np.all(np.isfinite(g["loss"]))
+    assert np.max(np.abs(occ - 1.0)) < 1e-3
+    pick = [0, 17, 63]
+    o = oracle.fwd_bwd_xf(lt[pick], [T] * 3, [U] * 3)
+    _assert_bit_exact({k: g[k][pick] for k in ("loss", "grad")}, o, ["loss", "grad"])
+
+
+def test_host_pointer_entry(gpu, oracle):
+    from ssnt_tts_amd import capi
+    lt = oracle.synth_log_trans(4, 30, 12, seed=1)
+    lo = np.random.default_rng(1).standard_normal((4, 30, 12)).astype(np.float32)
+    S, P = [30, 25, 12, 5], [12, 7, 12, 9]
+    h = capi.ssnt_fwd_bwd(lt, S, P, log_obs=lo, debug=True)
+    o = oracle.fwd_bwd_xf(lt, S, P, log_obs=lo, debug=True)
+    _assert_bit_exact(h, o, ["loss", "grad", "grad_obs", "log_alpha", "log_beta"])
+
+
+def test_autograd_function(gpu, oracle):
+    dev = torch.device("cuda:0")
+    lt = oracle.synth_log_trans(3, 20, 8, seed=4)
+    x = torch.from_numpy(lt).to(dev).requires_grad_(True)
+    S = torch.tensor([20, 15, 9], dtype=torch.int32, device=dev)
+    P = torch.tensor([8, 8, 4], dtype=torch.int32, device=dev)
+    loss = gpu.ssnt_lattice_loss(x, S, P)
+    w = torch.tensor([1.0, 2.0, 0.5], device=dev)
+    (loss * w).sum().backward()
+    o = oracle.fwd_bwd_xf(lt, [20, 15, 9], [8, 8, 4])
+    assert np.array_equal(loss.detach().cpu().numpy(), o["loss"])
+    want = o["grad"] * np.array([1.0, 2.0, 0.5], np.float32)[:, None, None, None]
+    assert np.array_equal(x.grad.cpu().numpy(), want)

@@ -1,0 +1,137 @@
+"""Pin the lattice forward-backward oracle (SURVEY.md 8(a) A11 -- not in the reference, so
+parity is pinned by independent references, not reference fixtures):
+
+  float64 C DP  == brute-force path enumeration   (tiny lattices, 1e-9)
+  float64 C DP  == torch float64 autograd DP      (small lattices, 1e-9)
+  split-exponent f32 oracle vs float64 C DP:
+      gradients           |d| <= 1e-5                 (north_star tolerance)
+      loss, log-alpha/beta |d| <= 1e-5 + 2^-23 |x|    (1e-5 plus the f32 rounding of x itself)
+"""
+import numpy as np
+import pytest
+
+import lattice_ref as LR
+
+F1 = 1  # FLAG_TERMINAL_EMIT
+
+
+def _close_log(a, b, atol=1e-5):
+    fin = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), fin) or np.all(~np.isfinite(a[~fin])), "inf pattern"
+    assert np.all(np.isneginf(a[~fin])), "unreachable cells must be -inf"
+    d = np.abs(a[fin].astype(np.float64) - b[fin])
+    tol = atol + 2.0 ** -23 * np.abs(b[fin])
+    assert np.all(d <= tol), f"max excess {np.max(d - tol)}"
+
+
+@pytest.mark.parametrize("obs", [False, True])
+@pytest.mark.parametrize("terminal", [True, False])
+@pytest.mark.parametrize("case", range(12))
+def test_f64_oracle_vs_brute_force(oracle, case, terminal, obs):
+    rng = np.random.default_rng(case)
+    T, U = 8, 4
+    S = int(rng.integers(1, T + 1))
+    P = int(rng.integers(1, U + 1))
+    lt = oracle.synth_log_trans(1, T, U, seed=case)
+    lo = (rng.standard_normal((1, T, U)) * 2 - 1).astype(np.float32) if obs else None
+    flags = F1 if terminal else 0
+    o = oracle.fwd_bwd_f64(lt, [S], [P], log_obs=lo, flags=flags)
+    loss, g, go = LR.brute_force(lt[0], S, P, None if lo is None else lo[0], terminal)
+    if np.isinf(loss):
+        assert np.isinf(o["loss"][0])
+        assert np.all(o["grad"] == 0)
+        return
+    assert abs(o["loss"][0] - loss) < 1e-9
+    assert np.max(np.abs(o["grad"][0] - g)) < 1e-9
+    if obs:
+        assert np.max(np.abs(o["grad_obs"][0] - go)) < 1e-9
+
+
+@pytest.mark.parametrize("obs", [False, True])
+@pytest.mark.parametrize("case", range(6))
+def test_f64_oracle_vs_torch_autograd(oracle, case, obs):
+    rng = np.random.default_rng(100 + case)
+    T, U = 30, 12
+    P = int(rng.integers(1, U + 1))
+    S = int(rng.integers(P, T + 1))
+    lt = oracle.synth_log_trans(1, T, U, seed=100 + case)
+    lo = (rng.standard_normal((1, T, U)) * 3).astype(np.float32) if obs else None
+    o = oracle.fwd_bwd_f64(lt, [S], [P], log_obs=lo)
+    loss, g, go = LR.torch_dp(lt[0], S, P, None if lo is None else lo[0], True)
+    assert abs(o["loss"][0] - loss) < 1e-9
+    assert np.max(np.abs(o["grad"][0] - g)) < 1e-9
+    if obs:
+        assert np.max(np.abs(o["grad_obs"][0] - go)) < 1e-9
+
+
+def _xf_vs_f64(oracle, lt, S, P, lo=None, flags=F1):
+    a = oracle.fwd_bwd_xf(lt, S, P, log_obs=lo, flags=flags, debug=True)
+    b = oracle.fwd_bwd_f64(lt, S, P, log_obs=lo, flags=flags)
+    fin = np.isfinite(b["loss"])
+    assert np.array_equal(np.isfinite(a["loss"]), fin)
+    _close_log(a["loss"][fin], b["loss"][fin])
+    assert np.max(np.abs(a["grad"] - b["grad"])) <= 1e-5
+    if lo is not None:
+        assert np.max(np.abs(a["grad_obs"] - b["grad_obs"])) <= 1e-5
+    _close_log(a["log_alpha"], b["log_alpha"])
+    _close_log(a["log_beta"], b["log_beta"])
+    return a, b
+
+
+def test_config1_single_utterance(oracle):
+    # BASELINE.json configs[0]: T=50 U=20 single utterance, CPU
+    lt = oracle.synth_log_trans(1, 50, 20, seed=0)
+    _xf_vs_f64(oracle, lt, [50], [20])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_ragged_batch(oracle, seed):
+    rng = np.random.default_rng(seed)
+    B, T, U = 6, 60, 24
+    P = rng.integers(U // 2, U + 1, size=B)
+    S = np.array([rng.integers(max(p, T // 2), T + 1) for p in P])
+    lt = oracle.synth_log_trans(B, T, U, seed=seed)
+    _xf_vs_f64(oracle, lt, S, P)
+
+
+def test_obs_and_nonterminal(oracle):
+    rng = np.random.default_rng(7)
+    lt = oracle.synth_log_trans(3, 40, 16, seed=7)
+    lo = (rng.standard_normal((3, 40, 16)) * 20 - 60).astype(np.float32)  # frame log-likelihoods
+    _xf_vs_f64(oracle, lt, [40, 33, 16], [16, 9, 16], lo=lo)
+    _xf_vs_f64(oracle, lt, [40, 33, 16], [16, 9, 16], lo=lo, flags=0)
+
+
+def test_edge_cases(oracle):
+    lt = oracle.synth_log_trans(7, 10, 5, seed=3)
+    S = [1, 10, 3, 5, 10, 0, 4]
+    P = [1, 1, 5, 5, 5, 1, 2]  # S=1,P=1 / P=1 / infeasible S<P / S==P / full / S=0 / small
+    a, b = _xf_vs_f64(oracle, lt, S, P)
+    assert np.isinf(a["loss"][2]) and np.isinf(a["loss"][5])
+    assert np.all(a["grad"][2] == 0) and np.all(a["grad"][5] == 0)
+    z = oracle.fwd_bwd_xf(lt, S, P, flags=F1 | 2)
+    assert z["loss"][2] == 0.0 and z["loss"][5] == 0.0  # zero_infinity
+
+
+def test_neg_inf_transitions(oracle):
+    # hard constraints: log(0) transitions make some paths impossible; all-impossible -> inf
+    lt = oracle.synth_log_trans(2, 12, 6, seed=5)
+    lt[0, :, 2, 1] = -np.inf  # never shift out of position 2
+    lt[1, 3:6, :, 0] = -np.inf
+    a, b = _xf_vs_f64(oracle, lt, [12, 12], [3, 6])
+    a, b = _xf_vs_f64(oracle, lt, [12, 12], [6, 6])
+    assert np.isinf(a["loss"][0]) and np.isinf(b["loss"][0])
+
+
+def test_posteriors_sum_to_one(oracle):
+    lt = oracle.synth_log_trans(2, 80, 30, seed=11)
+    a = oracle.fwd_bwd_xf(lt, [80, 64], [30, 21])
+    for b, S in enumerate([80, 64]):
+        occ = -(a["grad"][b, :S - 1].sum(axis=(1, 2)))
+        assert np.max(np.abs(occ - 1.0)) < 1e-5
+
+
+def test_large_magnitudes_long_form_slice(oracle):
+    # long-form statistics (|log alpha| in the thousands): f32 rounding dominates, see tolerance
+    lt = oracle.synth_log_trans(1, 600, 120, seed=2)
+    _xf_vs_f64(oracle, lt, [600], [120])
