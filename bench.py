@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark: lattice forward-backward (loss + grad) throughput on N MI355X GPUs.
+
+Workload (BASELINE.json configs[1], and configs[3] at N=8): per GPU B=256 utterances,
+T=200 steps x U=80 positions, f32 log_trans (B,T,U,2) = log_softmax over {emit, shift} of
+z ~ N(0, 1.5^2) (synthetic, generated on device, seed = rank). One step = one fused
+fwd-bwd launch through the C-ABI (ssnt_fwd_bwd_device) writing loss (B) and grad (B,T,U,2),
+plus the per-shard loss sum and, for N > 1, an RCCL all-reduce of that scalar over xGMI.
+Weak scaling: per-GPU work is fixed. value = all ranks' lattice cells / max-over-ranks time.
+
+roofline: algorithmic HBM bytes of the fwd-bwd kernel = 16 B/cell (read 2xf32 log_trans, write
+2xf32 grad) x cells per launch, over the kernel's average duration measured
+with HIP events on the launch stream inside the timed region; peak 8 TB/s (MI355X_MICROARCH.md).
+traffic: HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
+null when absent.
+cpu_baseline: the C oracle (oracle/ssnt_oracle.c, same split-exponent arithmetic; the reference
+has no forward-backward) on this host's cores, rank 0 at N=1 only.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "ssnt-tts-rust_amd"))
+
+import ssnt_tts_amd as S  # noqa: E402
+
+BASELINE = json.loads((ROOT / "BASELINE.json").read_text())
+PEAK_HBM_GBS = 8000.0
+BYTES_PER_CELL = 16
+
+
+def synth(B, T, U, seed, dev):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    z = torch.randn((B, T, U, 2), generator=g, device=dev, dtype=torch.float32) * 1.5
+    return torch.log_softmax(z, dim=-1).contiguous()
+
+
+def cpu_baseline(B, T, U):
+    """Time the C oracle on this host: repeated config-2 batches for ~2 s of wall time."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    lt = O.synth_log_trans(B, T, U, seed=0)
+    sl, pl = [T] * B, [U] * B
+    O.fwd_bwd_xf(lt[:8], sl[:8], pl[:8], n_threads=threads)  # warm-up
+    times = []
+    t_end = time.perf_counter() + 2.0
+    while len(times) < 3 or time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        O.fwd_bwd_xf(lt, sl, pl, n_threads=threads)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    t0 = time.perf_counter()
+    O.fwd_bwd_xf(lt[:16], sl[:16], pl[:16], n_threads=1)
+    single = 16 * T * U / (time.perf_counter() - t0)
+    return {"value": B * T * U / med, "unit": "cells/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} x full B={B} T={T} U={U} fwd-bwd+grad batches "
+                      f"(median {med * 1e3:.1f} ms/batch, {threads} OpenMP threads); "
+                      f"1 thread: {single:.3e} cells/s",
+            "single_thread_value": single}
+
+
+def pmc_traffic():
+    p = ROOT / "profiles" / "pmc_fwd_bwd.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256, help="utterances per GPU")
+    ap.add_argument("--T", type=int, default=200)
+    ap.add_argument("--U", type=int, default=80)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+
+    B, T, U = args.batch, args.T, args.U
+    lt = synth(B, T, U, seed=rank, dev=dev)
+    sl = torch.full((B,), T, dtype=torch.int32, device=dev)
+    pl = torch.full((B,), U, dtype=torch.int32, device=dev)
+    out = {"loss": torch.empty(B, device=dev), "grad": torch.empty((B, T, U, 2), device=dev),
+           "status": torch.zeros(1, dtype=torch.int32, device=dev)}
+    total = torch.zeros(1, device=dev)
+    # correctness/status check once through the full Python mirror, outside the timed region
+    r = S.ssnt_fwd_bwd(lt, sl, pl, out=out, check=True)
+    assert torch.isfinite(r["loss"]).all()
+
+    # the timed loop calls the C ABI directly (pointers bound once): the HIP events below then
+    # bracket exactly one kernel launch, and no Python wrapper work sits between launches
+    import ctypes
+    lib = S.load()
+    wsb = int(lib.ssnt_fwd_bwd_workspace_size(B, T, U))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    vp = ctypes.c_void_p
+    cargs = (vp(lt.data_ptr()), None, vp(sl.data_ptr()), vp(pl.data_ptr()), B, T, U, 1,
+             vp(out["loss"].data_ptr()), vp(out["grad"].data_ptr()), None, None, None,
+             vp(ws.data_ptr()) if wsb else None, wsb, None,
+             vp(torch.cuda.current_stream(dev).cuda_stream))
+
+    def launch():
+        rc = lib.ssnt_fwd_bwd_device(*cargs)
+        if rc != 0:
+            raise RuntimeError(f"ssnt_fwd_bwd_device: {S.status_string(rc)}")
+
+    def step():
+        launch()
+        torch.sum(out["loss"], dim=0, keepdim=True, out=total)
+        if dist:
+            torch.distributed.all_reduce(total)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record()
+        launch()
+        ev[i][1].record()
+        torch.sum(out["loss"], dim=0, keepdim=True, out=total)
+        if dist:
+            torch.distributed.all_reduce(total)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    cells_step = world * B * T * U
+    value = cells_step * K / elapsed
+    achieved = B * T * U * BYTES_PER_CELL / (kern_ms * 1e-3) / 1e9  # GB/s per GPU
+    if rank == 0:
+        res = {
+            "metric": BASELINE["metric"],
+            "value": value,
+            "unit": "cells/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (log_softmax of N(0,1.5^2) logits, generated on device)",
+            "config": {"workload": f"lattice fwd-bwd loss+grad, B={B}/GPU T={T} U={U} "
+                                   "(BASELINE configs[1]; configs[3] at N=8)",
+                       "global_batch": world * B, "T": T, "U": U,
+                       "parallelism": f"batch-sharded x{world}, RCCL loss all-reduce" if dist
+                       else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                         "traffic": pmc_traffic(),
+                         "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": B * T * U * BYTES_PER_CELL},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(B, T, U)
+        print(json.dumps(res), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -18,7 +18,9 @@ def _a(x, dt):
 
 
 def _p(a):
-    return ctypes.c_void_p(a.ctypes.data)
+    # data_as keeps a reference to the array, so temporaries built in the argument list stay
+    # alive for the duration of the call
+    return a.ctypes.data_as(ctypes.c_void_p)
 
 
 def ssnt_tts_beam_search_decode(h, log_prob_history, is_finished, t, u, max_t, beam_width):

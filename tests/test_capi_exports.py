@@ -1,0 +1,78 @@
+"""The C-ABI library (no GPU needed): it exists, loads, and exports exactly the symbols the
+public header declares -- including the seven unmangled reference symbols the TF ops bind
+(ssnt_tts_c/src/lib.rs:11,87,119,221,245,268,347). No compute calls here."""
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "ssnt_tts_c.h"
+LIB = ROOT / "ssnt-tts-rust_amd" / "lib" / "libssnt_tts_c.so"
+
+REFERENCE_SYMBOLS = [
+    "ssnt_tts_beam_search_decode", "ssnt_extract_best_beam_branch",
+    "ssnt_tts_v2_beam_search_decode", "ssnt_order_beam_branch", "ssnt_upsample_source_indexes",
+    "tone_latent_beam_search_decode", "tone_latent_levenshtein_edit_distance",
+]
+
+
+def header_functions():
+    txt = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    txt = re.sub(r"#.*", "", txt)
+    names = re.findall(r"\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", txt)
+    return sorted(set(n for n in names if n not in ("if", "while", "sizeof")))
+
+
+def test_header_declares_reference_symbols():
+    fns = header_functions()
+    for s in REFERENCE_SYMBOLS:
+        assert s in fns
+
+
+def test_library_exports_every_header_symbol():
+    assert LIB.exists(), "build the library first (make lib)"
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines() if " T " in line)
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, f"declared but not exported: {missing}"
+
+
+def test_ctypes_binding_matches_header():
+    from ssnt_tts_amd._lib import SIGNATURES, load
+    assert sorted(SIGNATURES) == header_functions()
+    lib = load()  # dlopen only; no HIP call
+    for name in SIGNATURES:
+        assert getattr(lib, name) is not None
+
+
+def test_reference_symbols_are_unmangled_c():
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True,
+                         check=True).stdout
+    for s in REFERENCE_SYMBOLS:
+        assert re.search(rf"\bT {s}$", out, flags=re.M), s
+
+
+def test_product_never_references_the_oracle():
+    # the product path must not link, load or import anything under oracle/
+    for p in (ROOT / "ssnt-tts-rust_amd").rglob("*"):
+        if p.is_file() and p.suffix in (".hip", ".h", ".cpp", ".c"):
+            code = re.sub(r"/\*.*?\*/|//[^\n]*", "", p.read_text(), flags=re.S)
+            assert "oracle" not in code, p
+        elif p.is_file() and p.suffix == ".py":
+            code = "\n".join(l.split("#")[0] for l in p.read_text().splitlines())
+            assert not re.search(r"^\s*(import|from)\s+oracle\b", code, flags=re.M), p
+            assert "libssnt_oracle" not in code, p
+    out = subprocess.run(["ldd", str(LIB)], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+
+
+def test_mirror_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import ssnt_tts_amd as S
+    with pytest.raises(RuntimeError):
+        S.ssnt_fwd_bwd(torch.zeros(1, 2, 2, 2), torch.ones(1), torch.ones(1))
