@@ -17,3 +17,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o write -- "${BENCH[@]}" \
   > "$OUT/write.log" 2>&1
 python3 tools/pmc_traffic.py "$OUT" "$TAG"
+# profiles/ is written on the box too, but only gpurun_out/ travels back: re-run
+# tools/pmc_traffic.py locally on gpurun_out/prof_<tag> to refresh the committed summaries.
