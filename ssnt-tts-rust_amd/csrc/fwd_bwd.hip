@@ -18,6 +18,8 @@
 //   stream out while the recurrence is still running.
 // Arithmetic: split-exponent xf (xf_math.h); bit-exact with oracle/ssnt_oracle.c.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "ssnt_internal.h"
 #include "xf_math.h"
@@ -25,20 +27,25 @@
 namespace ssnt {
 namespace {
 
-constexpr int kRing = 4;             // input prefetch depth (rows)
-constexpr size_t kLdsBudget = 150 * 1024;
+constexpr size_t kLdsBudget = 160 * 1024 - 256;  // one workgroup per CU may use ~all 160 KiB
+template <int K>
+constexpr int ring_depth() { return K <= 2 ? 8 : 4; }  // input prefetch depth (rows)
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// DPP wave shifts; lanes without a source keep `old` (bound_ctrl off), which is set to the
+// canonical xf zero, so lane 0 (shr) / lane 63 (shl) need no fix-up.
 __device__ __forceinline__ float shr1(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x138, 0xf, 0xf, false));
 }
 __device__ __forceinline__ int shr1(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, false);
+  return __builtin_amdgcn_update_dpp(XF_EZERO, x, 0x138, 0xf, 0xf, false);
 }
 __device__ __forceinline__ float shl1(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x130, 0xf, 0xf, false));
 }
 __device__ __forceinline__ int shl1(int x) {
-  return __builtin_amdgcn_update_dpp(0, x, 0x130, 0xf, 0xf, false);
+  return __builtin_amdgcn_update_dpp(XF_EZERO, x, 0x130, 0xf, 0xf, false);
 }
 
 template <int K, bool OBS>
@@ -47,83 +54,204 @@ struct Item {
   float ob[OBS ? K : 1];
 };
 
-// Load lane's slice of lt row `row` (and obs row `orow`) with rows clamped into [0,T).
-template <int K, bool OBS>
-__device__ __forceinline__ Item<K, OBS> load_item(const float* __restrict__ lt,
-                                                  const float* __restrict__ lo, int row,
-                                                  int orow, int T, int U, int lane) {
-  Item<K, OBS> it;
-  row = min(max(row, 0), T - 1);
-  const int p0 = K * lane;
-  const float2* src = reinterpret_cast<const float2*>(lt + ((size_t)row * U + p0) * 2);
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    float2 v = make_float2(0.0f, 0.0f);
-    if (p0 + j < U) v = src[j];
-    it.lt[2 * j] = v.x;
-    it.lt[2 * j + 1] = v.y;
-  }
-  if constexpr (OBS) {
-    orow = min(max(orow, 0), T - 1);
-    const float* osrc = lo + (size_t)orow * U + p0;
-#pragma unroll
-    for (int j = 0; j < K; ++j) it.ob[j] = (p0 + j < U) ? osrc[j] : 0.0f;
-  }
-  return it;
-}
-
 template <int K>
 struct XRow {
   float m[K];
   int e[K];
 };
 
-template <int K>
-__device__ __forceinline__ void store_row(xf* __restrict__ dst, const XRow<K>& r, int U, int lane) {
-  const int p0 = K * lane;
+// Lane slice of K consecutive positions, 4*N bytes, moved as one unit. VEC: U % K == 0 and
+// 16-byte aligned bases, so a lane's slice is either whole or entirely beyond U: one predicate,
+// widest loads. !VEC: per-element predicates (odd shapes only).
+template <int N>
+__device__ __forceinline__ void ld_vec(float* dst, const float* src) {
+  if constexpr (N % 4 == 0) {
 #pragma unroll
-  for (int j = 0; j < K; ++j)
-    if (p0 + j < U) dst[p0 + j] = xf{r.m[j], r.e[j]};
+    for (int q = 0; q < N / 4; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(src)[q];
+      dst[4 * q] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
+    }
+  } else if constexpr (N == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(src);
+    dst[0] = v.x; dst[1] = v.y;
+  } else {
+    dst[0] = src[0];
+  }
+}
+template <int N>
+__device__ __forceinline__ void st_vec(float* dst, const float* v) {
+  if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q)
+      reinterpret_cast<float4*>(dst)[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  } else if constexpr (N == 2) {
+    *reinterpret_cast<float2*>(dst) = make_float2(v[0], v[1]);
+  } else {
+    dst[0] = v[0];
+  }
 }
 
-template <int K>
+template <int K, bool OBS, bool VEC>
+__device__ __forceinline__ Item<K, OBS> load_item(const float* __restrict__ lt,
+                                                  const float* __restrict__ lo, int row,
+                                                  int orow, int T, int U, int lane) {
+  Item<K, OBS> it;
+  row = min(max(row, 0), T - 1);
+  const int p0 = K * lane;
+  const float* src = lt + ((size_t)row * U + p0) * 2;
+  if constexpr (VEC) {
+    if (p0 < U) {
+      ld_vec<2 * K>(it.lt, src);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2 * K; ++j) it.lt[j] = 0.0f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      float2 v = make_float2(0.0f, 0.0f);
+      if (p0 + j < U) v = reinterpret_cast<const float2*>(src)[j];
+      it.lt[2 * j] = v.x;
+      it.lt[2 * j + 1] = v.y;
+    }
+  }
+  if constexpr (OBS) {
+    orow = min(max(orow, 0), T - 1);
+    const float* osrc = lo + (size_t)orow * U + p0;
+    if constexpr (VEC) {
+      if (p0 < U) {
+        ld_vec<K>(it.ob, osrc);
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) it.ob[j] = 0.0f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) it.ob[j] = (p0 + j < U) ? osrc[j] : 0.0f;
+    }
+  }
+  return it;
+}
+
+template <int K, bool VEC>
+__device__ __forceinline__ void store_row(xf* __restrict__ dst, const XRow<K>& r, int U, int lane) {
+  const int p0 = K * lane;
+  if constexpr (VEC) {
+    if (p0 < U) {
+      float v[2 * K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        v[2 * j] = r.m[j];
+        v[2 * j + 1] = __builtin_bit_cast(float, r.e[j]);
+      }
+      st_vec<2 * K>(reinterpret_cast<float*>(dst + p0), v);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if (p0 + j < U) dst[p0 + j] = xf{r.m[j], r.e[j]};
+  }
+}
+
+template <int K, bool VEC>
 __device__ __forceinline__ XRow<K> load_row(const xf* __restrict__ src, int U, int lane) {
   XRow<K> r;
   const int p0 = K * lane;
+  if constexpr (VEC) {
+    float v[2 * K];
+    if (p0 < U) {
+      ld_vec<2 * K>(v, reinterpret_cast<const float*>(src + p0));
+    } else {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    xf v = xf_zero();
-    if (p0 + j < U) v = src[p0 + j];
-    r.m[j] = v.m;
-    r.e[j] = v.e;
+      for (int j = 0; j < K; ++j) {
+        v[2 * j] = 0.0f;
+        v[2 * j + 1] = __builtin_bit_cast(float, XF_EZERO);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      r.m[j] = v[2 * j];
+      r.e[j] = __builtin_bit_cast(int, v[2 * j + 1]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      xf v = xf_zero();
+      if (p0 + j < U) v = src[p0 + j];
+      r.m[j] = v.m;
+      r.e[j] = v.e;
+    }
   }
   return r;
 }
 
-template <int K>
+template <int K, bool VEC>
 __device__ __forceinline__ void store_grad_row(float* __restrict__ g, const float* ge,
                                                const float* gs, int U, int lane) {
   const int p0 = K * lane;
-  float2* dst = reinterpret_cast<float2*>(g + (size_t)p0 * 2);
+  float v[2 * K];
 #pragma unroll
-  for (int j = 0; j < K; ++j)
-    if (p0 + j < U) dst[j] = make_float2(ge[j], gs[j]);
+  for (int j = 0; j < K; ++j) {
+    v[2 * j] = ge[j];
+    v[2 * j + 1] = gs[j];
+  }
+  if constexpr (VEC) {
+    if (p0 < U) st_vec<2 * K>(g + (size_t)p0 * 2, v);
+  } else {
+    float2* dst = reinterpret_cast<float2*>(g + (size_t)p0 * 2);
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if (p0 + j < U) dst[j] = make_float2(v[2 * j], v[2 * j + 1]);
+  }
 }
 
-template <int K>
+template <int K, bool VEC>
 __device__ __forceinline__ void store_f_row(float* __restrict__ dst, const float* v, int U, int lane) {
   const int p0 = K * lane;
+  if constexpr (VEC) {
+    if (p0 < U) st_vec<K>(dst + p0, v);
+  } else {
 #pragma unroll
-  for (int j = 0; j < K; ++j)
-    if (p0 + j < U) dst[p0 + j] = v[j];
+    for (int j = 0; j < K; ++j)
+      if (p0 + j < U) dst[p0 + j] = v[j];
+  }
 }
 
-template <int K>
+template <int K, bool VEC>
 __device__ __forceinline__ void store_log_row(float* __restrict__ dst, const XRow<K>& r, int U, int lane) {
   float v[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) v[j] = xf_log(xf{r.m[j], r.e[j]});
-  store_f_row<K>(dst, v, U, lane);
+  store_f_row<K, VEC>(dst, v, U, lane);
+}
+
+// exp() of the (emit, shift) pair of one position as two unnormalized xf, with packed f32
+// FMAs (v_pk_fma_f32): the same per-element IEEE operations as xf_exp (xf_math.h). Inputs are
+// clamped into [XF_LOG_MIN, XF_LOG_MAX] for the arithmetic; dead elements are zeroed at the end.
+__device__ __forceinline__ void xf_exp_pair(float xe, float xs, bool ve, bool vs, float& me,
+                                            int& ee, float& ms, int& es) {
+  const bool le = ve && (xe >= XF_LOG_MIN);
+  const bool ls = vs && (xs >= XF_LOG_MIN);
+  f2 x;
+  x.x = __builtin_amdgcn_fmed3f(xe, XF_LOG_MIN, XF_LOG_MAX);
+  x.y = __builtin_amdgcn_fmed3f(xs, XF_LOG_MIN, XF_LOG_MAX);
+  const f2 t = x * (f2){kL2E, kL2E};
+  f2 n;
+  n.x = __builtin_rintf(t.x);
+  n.y = __builtin_rintf(t.y);
+  f2 r = __builtin_elementwise_fma(-n, (f2){kLN2HI, kLN2HI}, x);
+  r = __builtin_elementwise_fma(-n, (f2){kLN2LO, kLN2LO}, r);
+  f2 p = (f2){0x1.6da758p-10f, 0x1.6da758p-10f};
+  p = __builtin_elementwise_fma(p, r, (f2){0x1.126facp-7f, 0x1.126facp-7f});
+  p = __builtin_elementwise_fma(p, r, (f2){0x1.555464p-5f, 0x1.555464p-5f});
+  p = __builtin_elementwise_fma(p, r, (f2){0x1.555404p-3f, 0x1.555404p-3f});
+  p = __builtin_elementwise_fma(p, r, (f2){0x1p-1f, 0x1p-1f});
+  p = __builtin_elementwise_fma(p, r, (f2){0x1p+0f, 0x1p+0f});
+  p = __builtin_elementwise_fma(p, r, (f2){0x1p+0f, 0x1p+0f});
+  me = le ? p.x : 0.0f;
+  ee = le ? (int)n.x : XF_EZERO;
+  ms = ls ? p.y : 0.0f;
+  es = ls ? (int)n.y : XF_EZERO;
 }
 
 // Convert the lane's inputs of one row to xf: emit E, shift S (masked: p<P, shift p<P-1).
@@ -133,24 +261,26 @@ __device__ __forceinline__ void convert(const Item<K, OBS>& it, int P, int lane,
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int p = K * lane + j;
-    const xf e = xf_exp(it.lt[2 * j], p < P);
-    const xf s = xf_exp(it.lt[2 * j + 1], p < P - 1);
-    E.m[j] = e.m;
-    E.e[j] = e.e;
-    Sh.m[j] = s.m;
-    Sh.e[j] = s.e;
+    xf_exp_pair(it.lt[2 * j], it.lt[2 * j + 1], p < P, p < P - 1, E.m[j], E.e[j], Sh.m[j], Sh.e[j]);
   }
 }
 
 template <int K, bool OBS>
 __device__ __forceinline__ void convert_obs(const Item<K, OBS>& it, int P, int lane, XRow<K>& O) {
+  if constexpr (OBS) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    if constexpr (OBS) {
-      const xf o = xf_exp(it.ob[j], K * lane + j < P);
-      O.m[j] = o.m;
-      O.e[j] = o.e;
-    } else {
+    for (int j = 0; j + 1 < K; j += 2) {  // pairs of positions through the packed path
+      xf_exp_pair(it.ob[j], it.ob[j + 1], K * lane + j < P, K * lane + j + 1 < P, O.m[j], O.e[j],
+                  O.m[j + 1], O.e[j + 1]);
+    }
+    if constexpr (K % 2 == 1) {
+      const xf o = xf_exp(it.ob[K - 1], K * lane + K - 1 < P);
+      O.m[K - 1] = o.m;
+      O.e[K - 1] = o.e;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
       O.m[j] = 1.0f;
       O.e[j] = 0;
     }
@@ -160,8 +290,7 @@ __device__ __forceinline__ void convert_obs(const Item<K, OBS>& it, int P, int l
 // alpha[s+1] from alpha[s]: stay/shift products (returned for reuse by the gradients).
 template <int K, bool OBS>
 __device__ __forceinline__ void alpha_step(XRow<K>& A, const XRow<K>& E, const XRow<K>& Sh,
-                                           const XRow<K>& O, int lane, XRow<K>& stay,
-                                           XRow<K>& shft) {
+                                           const XRow<K>& O, XRow<K>& stay, XRow<K>& shft) {
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     stay.m[j] = A.m[j] * E.m[j];
@@ -169,12 +298,8 @@ __device__ __forceinline__ void alpha_step(XRow<K>& A, const XRow<K>& E, const X
     shft.m[j] = A.m[j] * Sh.m[j];
     shft.e[j] = A.e[j] + Sh.e[j];
   }
-  float lm = shr1(shft.m[K - 1]);
-  int le = shr1(shft.e[K - 1]);
-  if (lane == 0) {
-    lm = 0.0f;
-    le = XF_EZERO;
-  }
+  const float lm = shr1(shft.m[K - 1]);
+  const int le = shr1(shft.e[K - 1]);
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const float hm = (j == 0) ? lm : shft.m[j - 1];
@@ -194,7 +319,7 @@ __device__ __forceinline__ void alpha_step(XRow<K>& A, const XRow<K>& E, const X
 
 // Q = beta[s+1] (x obs[s+1]) and its right neighbour R = Q[p+1].
 template <int K, bool OBS>
-__device__ __forceinline__ void entering(const XRow<K>& Bn, const XRow<K>& O, int lane, XRow<K>& Q,
+__device__ __forceinline__ void entering(const XRow<K>& Bn, const XRow<K>& O, XRow<K>& Q,
                                          XRow<K>& R) {
 #pragma unroll
   for (int j = 0; j < K; ++j) {
@@ -206,12 +331,8 @@ __device__ __forceinline__ void entering(const XRow<K>& Bn, const XRow<K>& O, in
       Q.e[j] = Bn.e[j];
     }
   }
-  float rm = shl1(Q.m[0]);
-  int re = shl1(Q.e[0]);
-  if (lane == 63) {
-    rm = 0.0f;
-    re = XF_EZERO;
-  }
+  const float rm = shl1(Q.m[0]);
+  const int re = shl1(Q.e[0]);
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     R.m[j] = (j == K - 1) ? rm : Q.m[j + 1 < K ? j + 1 : 0];
@@ -230,8 +351,9 @@ __device__ __forceinline__ void beta_step(XRow<K>& Bt, const XRow<K>& E, const X
   }
 }
 
-template <int K, bool OBS, bool LDS>
+template <int K, bool OBS, bool LDS, bool VEC>
 __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
+  constexpr int kRing = ring_depth<K>();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int wave = threadIdx.x >> 6;
@@ -261,10 +383,10 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
         z[j] = 0.0f;
         ninf[j] = -__builtin_inff();
       }
-      if (g) store_grad_row<K>(g + (size_t)s * U * 2, z, z, U, lane);
-      if (go) store_f_row<K>(go + (size_t)s * U, z, U, lane);
-      if (la) store_f_row<K>(la + (size_t)s * U, ninf, U, lane);
-      if (lb) store_f_row<K>(lb + (size_t)s * U, ninf, U, lane);
+      if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, z, z, U, lane);
+      if (go) store_f_row<K, VEC>(go + (size_t)s * U, z, U, lane);
+      if (la) store_f_row<K, VEC>(la + (size_t)s * U, ninf, U, lane);
+      if (lb) store_f_row<K, VEC>(lb + (size_t)s * U, ninf, U, lane);
     }
   };
   const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
@@ -285,7 +407,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
 #pragma unroll
   for (int i = 0; i < kRing; ++i) {
     const int row = srow(i);
-    ring[i] = load_item<K, OBS>(lt, lo, row, row + 1, T, U, lane);
+    ring[i] = load_item<K, OBS, VEC>(lt, lo, row, row + 1, T, U, lane);
   }
   XRow<K> X;  // fwd: alpha row; bwd: beta row
   // ---------------- init ----------------
@@ -306,15 +428,15 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
         X.e[0] = 1;
       }
     }
-    store_row<K>(rows, X, U, lane);
-    if (la) store_log_row<K>(la, X, U, lane);
+    store_row<K, VEC>(rows, X, U, lane);
+    if (la) store_log_row<K, VEC>(la, X, U, lane);
   }
   const int r0 = fwd ? 0 : 1;               // bwd consumes stream slot 0 for its init
   const int r1 = fwd ? M : S - M;           // phase-1 end (exclusive)
   // bwd init uses ring slot 0 (row S-1)
   if (!fwd) {
     const Item<K, OBS> it = ring[0];
-    ring[0] = load_item<K, OBS>(lt, lo, srow(kRing), srow(kRing) + 1, T, U, lane);
+    ring[0] = load_item<K, OBS, VEC>(lt, lo, srow(kRing), srow(kRing) + 1, T, U, lane);
     XRow<K> E, Sh;
     convert<K, OBS>(it, P, lane, E, Sh);
 #pragma unroll
@@ -325,9 +447,9 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
       X.e[j] = last ? v.e : XF_EZERO;
     }
     const int s = S - 1;
-    if (s > M) store_row<K>(rows + (size_t)s * U, X, U, lane);
-    else store_row<K>(cutb, X, 64 * K, lane);
-    if (lb) store_log_row<K>(lb + (size_t)s * U, X, U, lane);
+    if (s > M) store_row<K, VEC>(rows + (size_t)s * U, X, U, lane);
+    else store_row<K, VEC>(cutb, X, 64 * K, lane);
+    if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
   }
   // ---------------- phase 1 ----------------
   for (int base = (r0 / kRing) * kRing; base < r1; base += kRing) {
@@ -337,23 +459,23 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
       if (r >= r0 && r < r1) {
         const Item<K, OBS> it = ring[i];
         const int nr = srow(r + kRing);
-        ring[i] = load_item<K, OBS>(lt, lo, nr, nr + 1, T, U, lane);
+        ring[i] = load_item<K, OBS, VEC>(lt, lo, nr, nr + 1, T, U, lane);
         XRow<K> E, Sh, O;
         convert<K, OBS>(it, P, lane, E, Sh);
         convert_obs<K, OBS>(it, P, lane, O);
         if (fwd) {  // alpha[r+1]
           XRow<K> stay, shft;
-          alpha_step<K, OBS>(X, E, Sh, O, lane, stay, shft);
-          store_row<K>(rows + (size_t)(r + 1) * U, X, U, lane);
-          if (la) store_log_row<K>(la + (size_t)(r + 1) * U, X, U, lane);
+          alpha_step<K, OBS>(X, E, Sh, O, stay, shft);
+          store_row<K, VEC>(rows + (size_t)(r + 1) * U, X, U, lane);
+          if (la) store_log_row<K, VEC>(la + (size_t)(r + 1) * U, X, U, lane);
         } else {  // beta[s], s = S-1-r
           const int s = S - 1 - r;
           XRow<K> Q, R;
-          entering<K, OBS>(X, O, lane, Q, R);
+          entering<K, OBS>(X, O, Q, R);
           beta_step<K>(X, E, Sh, Q, R);
-          if (s > M) store_row<K>(rows + (size_t)s * U, X, U, lane);
-          else store_row<K>(cutb, X, 64 * K, lane);
-          if (lb) store_log_row<K>(lb + (size_t)s * U, X, U, lane);
+          if (s > M) store_row<K, VEC>(rows + (size_t)s * U, X, U, lane);
+          else store_row<K, VEC>(cutb, X, 64 * K, lane);
+          if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
         }
       }
     }
@@ -412,7 +534,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
       if (r >= q0 && r < q1) {
         const Item<K, OBS> it = ring[i];
         const int nr = srow(r + kRing);
-        ring[i] = load_item<K, OBS>(lt, lo, nr, nr + 1, T, U, lane);
+        ring[i] = load_item<K, OBS, VEC>(lt, lo, nr, nr + 1, T, U, lane);
         XRow<K> E, Sh, O;
         convert<K, OBS>(it, P, lane, E, Sh);
         convert_obs<K, OBS>(it, P, lane, O);
@@ -421,8 +543,8 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
           const int s = r;  // transition s: alpha[s] (X) -> row s+1
           XRow<K> Q, R;
           if (s + 1 < S) {
-            const XRow<K> Bn = load_row<K>(rows + (size_t)(s + 1) * U, U, lane);
-            entering<K, OBS>(Bn, O, lane, Q, R);
+            const XRow<K> Bn = load_row<K, VEC>(rows + (size_t)(s + 1) * U, U, lane);
+            entering<K, OBS>(Bn, O, Q, R);
           } else {
 #pragma unroll
             for (int j = 0; j < K; ++j) {
@@ -434,33 +556,33 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
             }
           }
           if constexpr (OBS) {
-            const XRow<K> Bs = (s == M) ? load_row<K>(cutb, 64 * K, lane)
-                                        : load_row<K>(rows + (size_t)s * U, U, lane);
+            const XRow<K> Bs = (s == M) ? load_row<K, VEC>(cutb, 64 * K, lane)
+                                        : load_row<K, VEC>(rows + (size_t)s * U, U, lane);
 #pragma unroll
             for (int j = 0; j < K; ++j)
               gob[j] = xf_neg_post((X.m[j] * Bs.m[j]) * izm, X.e[j] + Bs.e[j] + ize);
           }
           XRow<K> stay, shft;
           XRow<K> Xn = X;
-          alpha_step<K, OBS>(Xn, E, Sh, O, lane, stay, shft);  // (stay/shft of alpha[s])
+          alpha_step<K, OBS>(Xn, E, Sh, O, stay, shft);  // (stay/shft of alpha[s])
 #pragma unroll
           for (int j = 0; j < K; ++j) {
             ge[j] = xf_neg_post((stay.m[j] * Q.m[j]) * izm, stay.e[j] + Q.e[j] + ize);
             gs[j] = xf_neg_post((shft.m[j] * R.m[j]) * izm, shft.e[j] + R.e[j] + ize);
           }
-          if (g) store_grad_row<K>(g + (size_t)s * U * 2, ge, gs, U, lane);
+          if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, ge, gs, U, lane);
           if constexpr (OBS) {
-            if (go) store_f_row<K>(go + (size_t)s * U, gob, U, lane);
+            if (go) store_f_row<K, VEC>(go + (size_t)s * U, gob, U, lane);
           }
           if (s + 1 < S) {
             X = Xn;
-            if (la) store_log_row<K>(la + (size_t)(s + 1) * U, X, U, lane);
+            if (la) store_log_row<K, VEC>(la + (size_t)(s + 1) * U, X, U, lane);
           }
         } else {
           const int s = S - 1 - r;  // transition s: beta[s+1] (X) -> beta[s]
           XRow<K> Q, R;
-          entering<K, OBS>(X, O, lane, Q, R);
-          const XRow<K> A = load_row<K>(rows + (size_t)s * U, U, lane);
+          entering<K, OBS>(X, O, Q, R);
+          const XRow<K> A = load_row<K, VEC>(rows + (size_t)s * U, U, lane);
 #pragma unroll
           for (int j = 0; j < K; ++j) {
             ge[j] = xf_neg_post(((A.m[j] * E.m[j]) * Q.m[j]) * izm, A.e[j] + E.e[j] + Q.e[j] + ize);
@@ -471,10 +593,10 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
 #pragma unroll
             for (int j = 0; j < K; ++j)
               gob[j] = xf_neg_post((A.m[j] * X.m[j]) * izm, A.e[j] + X.e[j] + ize);
-            if (go) store_f_row<K>(go + (size_t)s * U, gob, U, lane);
+            if (go) store_f_row<K, VEC>(go + (size_t)s * U, gob, U, lane);
           }
-          if (g) store_grad_row<K>(g + (size_t)s * U * 2, ge, gs, U, lane);
-          if (lb) store_log_row<K>(lb + (size_t)s * U, X, U, lane);
+          if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, ge, gs, U, lane);
+          if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
         }
       }
     }
@@ -482,46 +604,578 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
   fill_rows(S);
 }
 
+// =============================================================================================
+// Pipelined kernel: 2 chain waves + 2*NC converter waves per utterance.
+//   Converter waves (NC per direction) stream log_trans / log_obs rows through a deep register
+//   prefetch ring, convert them to split-exponent form (the exp of every input, the largest
+//   block of VALU work) and hand them to their chain through an R-slot LDS ring. The chain
+//   waves keep only the serial recurrence (+ the gradient rows in phase 2), at high priority.
+//   Hand-off (all LDS, one workgroup): converter writes slot -> release-store of its `done`
+//   counter; chain acquire-loads `done` only when it runs out of known-ready rows; chain
+//   publishes `kprog` (rows consumed; its slot reads completed before the store was issued) so
+//   converters can reuse slots. Every spin is bounded (status bit on timeout).
+// =============================================================================================
+constexpr int kStatusTimeout = 1 << 4;
+constexpr int kSpinLimit = 1 << 22;
+
+struct PipeCtl {
+  int done[2][4];  // per direction, per converter: rows of its share completed
+  int kprog[2];    // per direction: stream rows consumed by the chain
+  int bm_ready;    // beta[M] is in the cut buffer
+  int z_ready;     // Z is published
+  int pad[20];
+  xf z;
+  xf pad2;
+};
+
+__device__ __forceinline__ int lds_acquire(const int* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_relaxed(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// spin until *p >= target; returns the value seen (or target on timeout, with a status bit)
+__device__ __forceinline__ int spin_geq(const int* p, int target, int* status) {
+  int v = lds_acquire(p);
+  int n = 0;
+  while (v < target) {
+    __builtin_amdgcn_s_sleep(1);
+    v = lds_acquire(p);
+    if (++n > kSpinLimit) {
+      if (status && (threadIdx.x & 63) == 0) atomicOr(status, kStatusTimeout);
+      return target;
+    }
+  }
+  return v;
+}
+
+// converted-row slot: per position [E.m, E.e, S.m, S.e] (16 B), then obs [O.m, O.e] (8 B)
+template <int K, bool OBS, bool VEC>
+__device__ __forceinline__ void slot_write(float* es, float* ob, const XRow<K>& E,
+                                           const XRow<K>& Sh, const XRow<K>& O, int U, int lane) {
+  const int p0 = K * lane;
+  float v[4 * K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    v[4 * j] = E.m[j];
+    v[4 * j + 1] = __builtin_bit_cast(float, E.e[j]);
+    v[4 * j + 2] = Sh.m[j];
+    v[4 * j + 3] = __builtin_bit_cast(float, Sh.e[j]);
+  }
+  if constexpr (VEC) {
+    if (p0 < U) st_vec<4 * K>(es + 4 * p0, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if (p0 + j < U) st_vec<4>(es + 4 * (p0 + j), v + 4 * j);
+  }
+  if constexpr (OBS) {
+    float o[2 * K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      o[2 * j] = O.m[j];
+      o[2 * j + 1] = __builtin_bit_cast(float, O.e[j]);
+    }
+    if constexpr (VEC) {
+      if (p0 < U) st_vec<2 * K>(ob + 2 * p0, o);
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (p0 + j < U) st_vec<2>(ob + 2 * (p0 + j), o + 2 * j);
+    }
+  }
+}
+
+template <int K, bool OBS, bool VEC>
+__device__ __forceinline__ void slot_read(const float* es, const float* ob, XRow<K>& E,
+                                          XRow<K>& Sh, XRow<K>& O, int U, int lane) {
+  const int p0 = K * lane;
+  float v[4 * K];
+  if constexpr (VEC) {
+    if (p0 < U) {
+      ld_vec<4 * K>(v, es + 4 * p0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4 * K; ++j) v[j] = (j & 1) ? __builtin_bit_cast(float, XF_EZERO) : 0.0f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (p0 + j < U) {
+        ld_vec<4>(v + 4 * j, es + 4 * (p0 + j));
+      } else {
+        v[4 * j] = 0.0f;
+        v[4 * j + 1] = __builtin_bit_cast(float, XF_EZERO);
+        v[4 * j + 2] = 0.0f;
+        v[4 * j + 3] = __builtin_bit_cast(float, XF_EZERO);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    E.m[j] = v[4 * j];
+    E.e[j] = __builtin_bit_cast(int, v[4 * j + 1]);
+    Sh.m[j] = v[4 * j + 2];
+    Sh.e[j] = __builtin_bit_cast(int, v[4 * j + 3]);
+  }
+  if constexpr (OBS) {
+    float o[2 * K];
+    if constexpr (VEC) {
+      if (p0 < U) {
+        ld_vec<2 * K>(o, ob + 2 * p0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          o[2 * j] = 0.0f;
+          o[2 * j + 1] = __builtin_bit_cast(float, XF_EZERO);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        if (p0 + j < U) {
+          ld_vec<2>(o + 2 * j, ob + 2 * (p0 + j));
+        } else {
+          o[2 * j] = 0.0f;
+          o[2 * j + 1] = __builtin_bit_cast(float, XF_EZERO);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      O.m[j] = o[2 * j];
+      O.e[j] = __builtin_bit_cast(int, o[2 * j + 1]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      O.m[j] = 1.0f;
+      O.e[j] = 0;
+    }
+  }
+}
+
+template <int K>
+constexpr int conv_depth() { return K <= 2 ? 8 : (K <= 4 ? 4 : 2); }
+
+template <int K, bool OBS, bool LDS, bool VEC, int NC, int R>
+__global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int T = a.T, U = a.U;
+  const int S = a.step_len[b];
+  const int P = a.pos_len[b];
+  const bool term = (a.flags & SSNT_FLAG_TERMINAL_EMIT) != 0;
+  const size_t TU = (size_t)T * U;
+  const float* __restrict__ lt = a.log_trans + (size_t)b * TU * 2;
+  const float* __restrict__ lo = OBS ? a.log_obs + (size_t)b * TU : nullptr;
+  float* __restrict__ g = a.grad ? a.grad + (size_t)b * TU * 2 : nullptr;
+  float* __restrict__ go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
+  float* __restrict__ la = a.log_alpha ? a.log_alpha + (size_t)b * TU : nullptr;
+  float* __restrict__ lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
+
+  // LDS: control | cut buffer (64K xf) | rings [dir][R][slot] | storage rows (LDS mode)
+  PipeCtl* ctl = reinterpret_cast<PipeCtl*>(smem);
+  xf* cutb = reinterpret_cast<xf*>(smem + sizeof(PipeCtl));
+  const int es_words = ((U * 4 + 3) / 4) * 4;             // floats per E/S slot
+  const int ob_words = OBS ? ((U * 2 + 3) / 4) * 4 : 0;   // floats per obs slot
+  const int slot_words = es_words + ob_words;
+  float* rings = reinterpret_cast<float*>(cutb + 64 * K);
+  xf* rows = LDS ? reinterpret_cast<xf*>(rings + 2 * R * slot_words)
+                 : reinterpret_cast<xf*>(a.workspace) + (size_t)b * TU;
+
+  const bool feasible = S >= 1 && P >= 1 && S <= T && P <= U && S >= P;
+  const int nw = 2 + 2 * NC;
+  auto fill_rows = [&](int from, int w0, int wstep) {  // zero grads / -inf debug rows
+    for (int s = from + w0; s < T; s += wstep) {
+      float z[K], ninf[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        z[j] = 0.0f;
+        ninf[j] = -__builtin_inff();
+      }
+      if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, z, z, U, lane);
+      if (go) store_f_row<K, VEC>(go + (size_t)s * U, z, U, lane);
+      if (la) store_f_row<K, VEC>(la + (size_t)s * U, ninf, U, lane);
+      if (lb) store_f_row<K, VEC>(lb + (size_t)s * U, ninf, U, lane);
+    }
+  };
+  const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
+  if (!feasible) {
+    if ((S > T || P > U || S < 0 || P < 0) && a.status && threadIdx.x == 0)
+      atomicOr(a.status, kStatusBadLength);
+    fill_rows(0, wave, nw);
+    if (threadIdx.x == 0) a.loss[b] = inf_loss;
+    return;
+  }
+  if (threadIdx.x < 32) reinterpret_cast<int*>(ctl)[threadIdx.x] = 0;
+  __syncthreads();
+  const int M = (S - 1) >> 1;
+
+  if (wave >= 2) {
+    // ------------------------------ converter -----------------------------------------
+    const int d = (wave - 2) / NC;  // 0 = forward stream, 1 = backward stream
+    const int c = (wave - 2) % NC;
+    constexpr int D = conv_depth<K>();
+    float* ring_d = rings + (size_t)d * R * slot_words;
+    auto srow = [&](int r) { return d == 0 ? r : S - 1 - r; };
+    Item<K, OBS> pf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int row = srow(c + NC * i);
+      pf[i] = load_item<K, OBS, VEC>(lt, lo, row, row + 1, T, U, lane);
+    }
+    int kseen = 0;
+    const int nmine = (S - c + NC - 1) / NC;  // my stream rows: c, c+NC, ...
+    for (int base = 0; base < nmine; base += D) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const int k = base + i;
+        if (k < nmine) {
+          const int r = c + NC * k;
+          const Item<K, OBS> it = pf[i];
+          const int nrow = srow(r + NC * D);
+          pf[i] = load_item<K, OBS, VEC>(lt, lo, nrow, nrow + 1, T, U, lane);
+          XRow<K> E, Sh, O;
+          convert<K, OBS>(it, P, lane, E, Sh);
+          convert_obs<K, OBS>(it, P, lane, O);
+          if (r - R >= kseen) kseen = spin_geq(&ctl->kprog[d], r - R + 1, a.status);
+          float* slot = ring_d + (size_t)(r % R) * slot_words;
+          slot_write<K, OBS, VEC>(slot, slot + es_words, E, Sh, O, U, lane);
+          if (lane == 0) lds_release(&ctl->done[d][c], k + 1);
+        }
+      }
+    }
+    // idle converters fill the rows beyond S
+    fill_rows(S, wave - 2, 2 * NC);
+    return;
+  }
+
+  // ------------------------------ chains -------------------------------------------------
+  __builtin_amdgcn_s_setprio(2);
+  const bool fwd = (wave == 0);
+  const int d = fwd ? 0 : 1;
+  const float* ring_d = rings + (size_t)d * R * slot_words;
+  int ready = 0;  // stream rows known converted
+  auto wait_row = [&](int r) {
+    if (r < ready) return;
+    int mn = 0x7fffffff;
+    for (int c = 0; c < NC; ++c) {
+      // converter c has produced rows c, c+NC, ..., c+NC*(done-1): first missing c+NC*done
+      const int need = (r - c + NC) / NC;  // rows of c that must be done to cover r
+      int dn = lds_acquire(&ctl->done[d][c]);
+      if (c + NC * dn <= r && need > 0) dn = spin_geq(&ctl->done[d][c], need, a.status);
+      mn = min(mn, c + NC * dn);
+    }
+    ready = mn;
+  };
+  auto read_row = [&](int r, XRow<K>& E, XRow<K>& Sh, XRow<K>& O) {
+    wait_row(r);
+    const float* slot = ring_d + (size_t)(r % R) * slot_words;
+    slot_read<K, OBS, VEC>(slot, slot + es_words, E, Sh, O, U, lane);
+  };
+  auto consumed = [&](int r) {  // slot of stream row r may be reused (its reads are done)
+    if (lane == 0) lds_release(&ctl->kprog[d], r + 1);
+  };
+
+  XRow<K> X;
+  if (fwd) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      X.m[j] = 0.0f;
+      X.e[j] = XF_EZERO;
+    }
+    if (lane == 0) {
+      if constexpr (OBS) {
+        const xf o = xf_exp(lo[0], true);
+        const xf n = xf_norm(o.m, o.e);
+        X.m[0] = n.m;
+        X.e[0] = n.e;
+      } else {
+        X.m[0] = 0.5f;
+        X.e[0] = 1;
+      }
+    }
+    store_row<K, VEC>(rows, X, U, lane);
+    if (la) store_log_row<K, VEC>(la, X, U, lane);
+    // phase 1: alpha[1..M]
+    for (int r = 0; r < M; ++r) {
+      XRow<K> E, Sh, O, stay, shft;
+      read_row(r, E, Sh, O);
+      alpha_step<K, OBS>(X, E, Sh, O, stay, shft);
+      consumed(r);
+      store_row<K, VEC>(rows + (size_t)(r + 1) * U, X, U, lane);
+      if (la) store_log_row<K, VEC>(la + (size_t)(r + 1) * U, X, U, lane);
+    }
+  } else {
+    // init from stream row 0 (= row S-1): terminal emit
+    {
+      XRow<K> E, Sh, O;
+      read_row(0, E, Sh, O);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const bool last = (K * lane + j) == P - 1;
+        xf v = term ? xf_norm(E.m[j], E.e[j]) : xf{0.5f, 1};
+        X.m[j] = last ? v.m : 0.0f;
+        X.e[j] = last ? v.e : XF_EZERO;
+      }
+      consumed(0);
+      const int s = S - 1;
+      if (s > M) store_row<K, VEC>(rows + (size_t)s * U, X, U, lane);
+      else store_row<K, VEC>(cutb, X, 64 * K, lane);
+      if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
+    }
+    for (int r = 1; r < S - M; ++r) {  // beta[S-2..M]
+      const int s = S - 1 - r;
+      XRow<K> E, Sh, O, Q, R_;
+      read_row(r, E, Sh, O);
+      entering<K, OBS>(X, O, Q, R_);
+      beta_step<K>(X, E, Sh, Q, R_);
+      consumed(r);
+      if (s > M) store_row<K, VEC>(rows + (size_t)s * U, X, U, lane);
+      else store_row<K, VEC>(cutb, X, 64 * K, lane);
+      if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
+    }
+    if (lane == 0) lds_release(&ctl->bm_ready, 1);
+  }
+  // ------------------------------ cut ----------------------------------------------------
+  if (fwd) {
+    spin_geq(&ctl->bm_ready, 1, a.status);
+    float wm[K];
+    int we[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const xf cb = cutb[K * lane + j];
+      wm[j] = X.m[j] * cb.m;
+      we[j] = X.e[j] + cb.e;
+    }
+#pragma unroll
+    for (int len = K; len > 1; len >>= 1) {
+#pragma unroll
+      for (int i = 0; i < len / 2; ++i) {
+        const xf r = xf_add(wm[2 * i], we[2 * i], wm[2 * i + 1], we[2 * i + 1]);
+        wm[i] = r.m;
+        we[i] = r.e;
+      }
+    }
+    xf z{wm[0], we[0]};
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const float om = __shfl_xor(z.m, off);
+      const int oe = __shfl_xor(z.e, off);
+      z = xf_add(z.m, z.e, om, oe);
+    }
+    if (lane == 0) {
+      ctl->z = z;
+      lds_release(&ctl->z_ready, 1);
+    }
+  } else {
+    spin_geq(&ctl->z_ready, 1, a.status);
+  }
+  const xf Z = ctl->z;
+  if (Z.m == 0.0f) {  // numerically infeasible: release the converters, zero everything
+    if (lane == 0) lds_relaxed(&ctl->kprog[d], 0x3fffffff);
+    fill_rows(0, wave, 2);
+    if (threadIdx.x == 0) a.loss[b] = inf_loss;
+    return;
+  }
+  if (fwd && lane == 0) a.loss[b] = 0.0f - xf_log(Z);
+  const float izm = 1.0f / Z.m;
+  const int ize = -Z.e;
+  // ------------------------------ phase 2 ------------------------------------------------
+  if (fwd) {
+    for (int s = M; s < S; ++s) {  // transition s: alpha[s] (X) -> row s+1
+      XRow<K> E, Sh, O, Q, R_;
+      read_row(s, E, Sh, O);
+      if (s + 1 < S) {
+        const XRow<K> Bn = load_row<K, VEC>(rows + (size_t)(s + 1) * U, U, lane);
+        entering<K, OBS>(Bn, O, Q, R_);
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const bool last = term && (K * lane + j) == P - 1;
+          Q.m[j] = last ? 1.0f : 0.0f;
+          Q.e[j] = last ? 0 : XF_EZERO;
+          R_.m[j] = 0.0f;
+          R_.e[j] = XF_EZERO;
+        }
+      }
+      float ge[K], gs[K];
+      if constexpr (OBS) {
+        const XRow<K> Bs = (s == M) ? load_row<K, VEC>(cutb, 64 * K, lane)
+                                    : load_row<K, VEC>(rows + (size_t)s * U, U, lane);
+        float gob[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          gob[j] = xf_neg_post((X.m[j] * Bs.m[j]) * izm, X.e[j] + Bs.e[j] + ize);
+        if (go) store_f_row<K, VEC>(go + (size_t)s * U, gob, U, lane);
+      }
+      XRow<K> stay, shft;
+      XRow<K> Xn = X;
+      alpha_step<K, OBS>(Xn, E, Sh, O, stay, shft);
+      consumed(s);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        ge[j] = xf_neg_post((stay.m[j] * Q.m[j]) * izm, stay.e[j] + Q.e[j] + ize);
+        gs[j] = xf_neg_post((shft.m[j] * R_.m[j]) * izm, shft.e[j] + R_.e[j] + ize);
+      }
+      if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, ge, gs, U, lane);
+      if (s + 1 < S) {
+        X = Xn;
+        if (la) store_log_row<K, VEC>(la + (size_t)(s + 1) * U, X, U, lane);
+      }
+    }
+  } else {
+    for (int r = S - M; r < S; ++r) {  // transition s = S-1-r: beta[s+1] (X) -> beta[s]
+      const int s = S - 1 - r;
+      XRow<K> E, Sh, O, Q, R_;
+      read_row(r, E, Sh, O);
+      entering<K, OBS>(X, O, Q, R_);
+      const XRow<K> A = load_row<K, VEC>(rows + (size_t)s * U, U, lane);
+      float ge[K], gs[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        ge[j] = xf_neg_post(((A.m[j] * E.m[j]) * Q.m[j]) * izm, A.e[j] + E.e[j] + Q.e[j] + ize);
+        gs[j] = xf_neg_post(((A.m[j] * Sh.m[j]) * R_.m[j]) * izm, A.e[j] + Sh.e[j] + R_.e[j] + ize);
+      }
+      beta_step<K>(X, E, Sh, Q, R_);
+      consumed(r);
+      if constexpr (OBS) {
+        float gob[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          gob[j] = xf_neg_post((A.m[j] * X.m[j]) * izm, A.e[j] + X.e[j] + ize);
+        if (go) store_f_row<K, VEC>(go + (size_t)s * U, gob, U, lane);
+      }
+      if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, ge, gs, U, lane);
+      if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
+    }
+  }
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <int K, bool OBS, bool LDS, bool VEC>
+int launch_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
+  auto kern = k_fwd_bwd<K, OBS, LDS, VEC>;
+  if (lds > 64 * 1024) {  // dynamic LDS above 64 KiB needs the attribute (idempotent)
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(128), lds, st, a);
+  return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
+}
+
 template <int K, bool OBS>
 int launch_k(const FwdBwdArgs& a, hipStream_t st) {
   const size_t head = (size_t)(64 * K + 2) * sizeof(xf);
   const size_t rows = (size_t)a.T * a.U * sizeof(xf);
-  if (head + rows <= kLdsBudget) {
-    const size_t lds = head + rows;
-    auto kern = k_fwd_bwd<K, OBS, true>;
-    static bool attr_set = false;  // dynamic LDS above 64 KiB needs the attribute
+  const bool lds = head + rows <= kLdsBudget;
+  if (!lds && (a.workspace == nullptr || a.workspace_bytes < fwd_bwd_workspace_bytes(a.B, a.T, a.U)))
+    return SSNT_ERR_WORKSPACE;
+  // whole lane slices (U % K == 0) and 16-byte aligned tensors -> widest branch-free accesses
+  const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
+                   aligned16(a.grad) && aligned16(a.grad_obs) && aligned16(a.log_alpha) &&
+                   aligned16(a.log_beta) && aligned16(a.workspace);
+  const size_t shm = lds ? head + rows : head;
+  if (lds)
+    return vec ? launch_kernel<K, OBS, true, true>(a, shm, st) : launch_kernel<K, OBS, true, false>(a, shm, st);
+  return vec ? launch_kernel<K, OBS, false, true>(a, shm, st) : launch_kernel<K, OBS, false, false>(a, shm, st);
+}
+
+constexpr int kPipeNC = 2;  // converter waves per direction
+constexpr int kPipeR = 8;   // ring slots per direction
+
+inline size_t pipe_head_bytes(int K, int U, bool obs) {
+  const size_t es = ((size_t)U * 4 + 3) / 4 * 4, ob = obs ? ((size_t)U * 2 + 3) / 4 * 4 : 0;
+  return sizeof(PipeCtl) + (size_t)64 * K * sizeof(xf) + 2 * (size_t)kPipeR * (es + ob) * 4;
+}
+
+template <int K, bool OBS, bool LDS, bool VEC>
+int launch_pipe_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
+  auto kern = k_fwd_bwd_pipe<K, OBS, LDS, VEC, kPipeNC, kPipeR>;
+  if (lds > 64 * 1024) {
+    static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
       attr_set = true;
     }
-    hipLaunchKernelGGL(kern, dim3(a.B), dim3(128), lds, st, a);
-  } else {
-    if (a.workspace == nullptr || a.workspace_bytes < fwd_bwd_workspace_bytes(a.B, a.T, a.U))
-      return SSNT_ERR_WORKSPACE;
-    hipLaunchKernelGGL((k_fwd_bwd<K, OBS, false>), dim3(a.B), dim3(128), head, st, a);
   }
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(64 * (2 + 2 * kPipeNC)), lds, st, a);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
+}
+
+template <int K, bool OBS>
+int launch_pipe(const FwdBwdArgs& a, hipStream_t st) {
+  const size_t head = pipe_head_bytes(K, a.U, OBS);
+  const size_t rows = (size_t)a.T * a.U * sizeof(xf);
+  if (head > kLdsBudget) return SSNT_ERR_UNSUPPORTED;
+  const bool lds = head + rows <= kLdsBudget;
+  if (!lds && (a.workspace == nullptr || a.workspace_bytes < (size_t)a.B * rows))
+    return SSNT_ERR_WORKSPACE;
+  const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
+                   aligned16(a.grad) && aligned16(a.grad_obs) && aligned16(a.log_alpha) &&
+                   aligned16(a.log_beta) && aligned16(a.workspace);
+  const size_t shm = lds ? head + rows : head;
+  if (lds)
+    return vec ? launch_pipe_kernel<K, OBS, true, true>(a, shm, st)
+               : launch_pipe_kernel<K, OBS, true, false>(a, shm, st);
+  return vec ? launch_pipe_kernel<K, OBS, false, true>(a, shm, st)
+             : launch_pipe_kernel<K, OBS, false, false>(a, shm, st);
+}
+
+int g_variant = -1;  // -1: not chosen yet (env SSNT_FWD_BWD_KERNEL), 0 pipelined, 1 simple
+
+inline bool use_simple_kernel() {
+  if (g_variant < 0) {
+    const char* e = getenv("SSNT_FWD_BWD_KERNEL");
+    g_variant = (e && strcmp(e, "simple") == 0) ? 1 : 0;
+  }
+  return g_variant == 1;
 }
 
 template <bool OBS>
 int launch_obs(const FwdBwdArgs& a, hipStream_t st) {
-  if (a.U <= 64) return launch_k<1, OBS>(a, st);
-  if (a.U <= 128) return launch_k<2, OBS>(a, st);
-  if (a.U <= 256) return launch_k<4, OBS>(a, st);
-  if (a.U <= 512) return launch_k<8, OBS>(a, st);
-  if (a.U <= 1024) return launch_k<16, OBS>(a, st);
+  if (use_simple_kernel()) {
+    if (a.U <= 64) return launch_k<1, OBS>(a, st);
+    if (a.U <= 128) return launch_k<2, OBS>(a, st);
+    if (a.U <= 256) return launch_k<4, OBS>(a, st);
+    if (a.U <= 512) return launch_k<8, OBS>(a, st);
+    return SSNT_ERR_UNSUPPORTED;
+  }
+  if (a.U <= 64) return launch_pipe<1, OBS>(a, st);
+  if (a.U <= 128) return launch_pipe<2, OBS>(a, st);
+  if (a.U <= 256) return launch_pipe<4, OBS>(a, st);
+  if (a.U <= 512) return launch_pipe<8, OBS>(a, st);
   return SSNT_ERR_UNSUPPORTED;
 }
 
 }  // namespace
 
 size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
-  const int K = U <= 64 ? 1 : U <= 128 ? 2 : U <= 256 ? 4 : U <= 512 ? 8 : 16;
-  const size_t head = (size_t)(64 * K + 2) * sizeof(xf);
+  // conservative over both kernels and with/without log_obs: rows go to global memory when
+  // the largest LDS head plus T*U*8 bytes of rows does not fit
+  const int K = U <= 64 ? 1 : U <= 128 ? 2 : U <= 256 ? 4 : 8;
+  const size_t head = pipe_head_bytes(K, U, true);
   const size_t rows = (size_t)T * U * sizeof(xf);
   if (head + rows <= kLdsBudget) return 0;
   return (size_t)B * rows;
+}
+
+int set_fwd_bwd_variant(int v) {
+  if (v < 0 || v > 1) return SSNT_ERR_INVALID_ARG;
+  g_variant = v;
+  return SSNT_OK;
 }
 
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t st) {

@@ -35,6 +35,7 @@ struct FwdBwdArgs {
 };
 size_t fwd_bwd_workspace_bytes(int B, int T, int U);
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
+int set_fwd_bwd_variant(int v);
 
 // ---- beam-search decode (decode.hip) ----
 enum class Variant : int { V1 = 0, V2 = 1, Tone = 2 };

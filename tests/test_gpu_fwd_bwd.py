@@ -15,6 +15,15 @@ pytestmark = pytest.mark.gpu
 F_TERM, F_ZINF = 1, 2
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["pipelined", "simple"])
+def kernel_variant(request, gpu):
+    """Every parity case runs on both kernel variants (they must be bit-identical)."""
+    lib = gpu.load()
+    assert lib.ssnt_fwd_bwd_set_variant(request.param) == 0
+    yield request.param
+    lib.ssnt_fwd_bwd_set_variant(0)
+
+
 def _run_gpu(gpu, lt, S, P, lo=None, flags=F_TERM, debug=True):
     dev = torch.device("cuda:0")
     r = gpu.ssnt_fwd_bwd(torch.from_numpy(lt).to(dev), torch.tensor(S, dtype=torch.int32, device=dev),
