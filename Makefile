@@ -18,6 +18,9 @@ HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/decode.hip $(CSRC)/capi.hip
 HIP_HDRS  := $(wildcard $(CSRC)/*.h) include/ssnt_tts_c.h
 HIP_OBJS  := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(HIP_SRCS))
 
+DIAGDIR   := $(LIBDIR)/diag
+DIAG_OBJS := $(patsubst $(CSRC)/%.hip,$(DIAGDIR)/obj/%.o,$(HIP_SRCS))
+
 all: lib oracle
 
 lib: $(LIB)
@@ -30,6 +33,14 @@ $(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 $(LIB): $(HIP_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(HIP_OBJS) -Wl,-soname,libssnt_tts_c.so
 
+# diagnostic build with in-kernel s_memtime stamps (tools/diag_fwd_bwd.py); never the product
+lib-diag: $(DIAGDIR)/libssnt_tts_c.so
+$(DIAGDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DSSNT_DIAG -c $< -o $@
+$(DIAGDIR)/libssnt_tts_c.so: $(DIAG_OBJS)
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(DIAG_OBJS) -Wl,-soname,libssnt_tts_c.so
+
 $(ORACLE): oracle/ssnt_oracle.c
 	@mkdir -p $(dir $@)
 	gcc -O3 -std=c11 -fopenmp -ffp-contract=off -fPIC -shared -Wall -o $@ $< -lm
@@ -37,4 +48,4 @@ $(ORACLE): oracle/ssnt_oracle.c
 clean:
 	rm -rf $(LIBDIR) oracle/build
 
-.PHONY: all lib oracle clean
+.PHONY: all lib lib-diag oracle clean

@@ -122,9 +122,10 @@ int ssnt_version(char *buf, size_t len);
  * default); `workspace` must hold ssnt_fwd_bwd_workspace_size() bytes (may be 0 -> NULL);
  * `status` (device int, may be NULL) receives error bits. Asynchronous. */
 size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos);
-/* Kernel variant for the forward-backward (results are bit-identical): 0 = pipelined
- * (converter waves feed two chain waves through LDS rings; default), 1 = simple two-wave
- * kernel. Process-wide; also settable with env SSNT_FWD_BWD_KERNEL=simple. For A/B timing. */
+/* Kernel variant for the forward-backward (results are bit-identical): 0 = pipelined, three
+ * converter waves per direction feed two chain waves through LDS rings (default); 1 = simple
+ * two-wave kernel; 2 = pipelined with two converters per direction. Process-wide; env
+ * SSNT_FWD_BWD_KERNEL=simple selects 1 at first use. For A/B timing and debugging. */
 int ssnt_fwd_bwd_set_variant(int variant);
 int ssnt_fwd_bwd_device(const float *log_trans, const float *log_obs, const int *step_len,
                         const int *pos_len, int batch, int max_steps, int max_pos, int flags,

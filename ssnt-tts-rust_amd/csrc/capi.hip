@@ -454,6 +454,9 @@ void tone_latent_levenshtein_edit_distance(const int* a, const int* b, const int
 
 int ssnt_fwd_bwd_set_variant(int variant) { return set_fwd_bwd_variant(variant); }
 
+// diagnostic builds (make lib-diag) only; not part of the public header
+int ssnt_diag_read(void* host, size_t bytes) { return diag_read(host, bytes); }
+
 size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos) {
   if (batch <= 0 || max_steps <= 0 || max_pos <= 0) return 0;
   return fwd_bwd_workspace_bytes(batch, max_steps, max_pos);

@@ -21,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "buffer_ops.h"
 #include "ssnt_internal.h"
 #include "xf_math.h"
 
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
   constexpr int kRing = ring_depth<K>();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR rsrcs
   const int lane = threadIdx.x & 63;
   const int T = a.T, U = a.U;
   const int S = a.step_len[b];
@@ -605,18 +606,35 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
 }
 
 // =============================================================================================
-// Pipelined kernel: 2 chain waves + 2*NC converter waves per utterance.
+// Pipelined kernel (VEC shapes: U % K == 0, 16-byte aligned tensors):
+//   2 chain waves + 2*NC converter waves per utterance (one workgroup).
 //   Converter waves (NC per direction) stream log_trans / log_obs rows through a deep register
 //   prefetch ring, convert them to split-exponent form (the exp of every input, the largest
 //   block of VALU work) and hand them to their chain through an R-slot LDS ring. The chain
 //   waves keep only the serial recurrence (+ the gradient rows in phase 2), at high priority.
-//   Hand-off (all LDS, one workgroup): converter writes slot -> release-store of its `done`
-//   counter; chain acquire-loads `done` only when it runs out of known-ready rows; chain
-//   publishes `kprog` (rows consumed; its slot reads completed before the store was issued) so
-//   converters can reuse slots. Every spin is bounded (status bit on timeout).
+// Every per-step memory access in the chain is unpredicated straight-line code, so the
+// compiler can schedule the whole step as one block: global rows use buffer instructions whose
+// hardware range check drops / zero-fills lanes past U; LDS accesses of lanes past U are
+// redirected to a junk (stores) or canonical-zero (loads) area by an address select.
+// Hand-off (all LDS, one workgroup): converter writes a slot, then release-stores its `done`
+// counter; the chain acquire-loads `done` only when it runs out of known-ready rows. The chain
+// returns a slot by storing `kprog` with a value that data-depends on the slot's contents
+// (so the store cannot issue before the slot reads returned; LDS executes a wave's DS ops in
+// order). Every spin is bounded (status bit on timeout).
 // =============================================================================================
 constexpr int kStatusTimeout = 1 << 4;
 constexpr int kSpinLimit = 1 << 22;
+
+// Diagnostic build only (-DSSNT_DIAG, `make lib-diag`): s_memtime stamps per role, read back with
+// ssnt_diag_read(). Layout: g_diag[b*4 + role][8], role 0 fwd chain, 1 bwd chain, 2/3 first
+// fwd/bwd converter. Slots: 0 total, 1 wait-for-rows (chain) / wait-for-slot (conv),
+// 2 waits, 3 cut wait, 4 phase-1 end. Never present in the product build.
+#ifdef SSNT_DIAG
+__device__ unsigned long long g_diag[4096 * 4][8];
+#define DIAG_T() __builtin_amdgcn_s_memtime()
+#else
+#define DIAG_T() 0ull
+#endif
 
 struct PipeCtl {
   int done[2][4];  // per direction, per converter: rows of its share completed
@@ -631,18 +649,19 @@ struct PipeCtl {
 __device__ __forceinline__ int lds_acquire(const int* p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
+// uniform counter stores: every lane stores the same value (one unpredicated ds_write)
 __device__ __forceinline__ void lds_release(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_relaxed(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// spin until *p >= target; returns the value seen (or target on timeout, with a status bit)
+template <bool SLEEP = true>
 __device__ __forceinline__ int spin_geq(const int* p, int target, int* status) {
   int v = lds_acquire(p);
   int n = 0;
   while (v < target) {
-    __builtin_amdgcn_s_sleep(1);
+    if constexpr (SLEEP) __builtin_amdgcn_s_sleep(1);
     v = lds_acquire(p);
     if (++n > kSpinLimit) {
       if (status && (threadIdx.x & 63) == 0) atomicOr(status, kStatusTimeout);
@@ -652,158 +671,157 @@ __device__ __forceinline__ int spin_geq(const int* p, int target, int* status) {
   return v;
 }
 
-// converted-row slot: per position [E.m, E.e, S.m, S.e] (16 B), then obs [O.m, O.e] (8 B)
-template <int K, bool OBS, bool VEC>
-__device__ __forceinline__ void slot_write(float* es, float* ob, const XRow<K>& E,
-                                           const XRow<K>& Sh, const XRow<K>& O, int U, int lane) {
-  const int p0 = K * lane;
-  float v[4 * K];
+// raw buffer over [base, base+bytes): out-of-range lanes read 0 / drop their stores.
+// `base` must be wave-uniform (the descriptor lives in SGPRs).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+// N floats at byte offset voff of a buffer range
+template <int N>
+__device__ __forceinline__ void buf_ld(float* dst, __amdgpu_buffer_rsrc_t r, int voff) {
+  if constexpr (N % 4 == 0) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    v[4 * j] = E.m[j];
-    v[4 * j + 1] = __builtin_bit_cast(float, E.e[j]);
-    v[4 * j + 2] = Sh.m[j];
-    v[4 * j + 3] = __builtin_bit_cast(float, Sh.e[j]);
-  }
-  if constexpr (VEC) {
-    if (p0 < U) st_vec<4 * K>(es + 4 * p0, v);
+    for (int q = 0; q < N / 4; ++q) {
+      const f32x4 v = rbuf_ld4(r, voff + 16 * q, 0, 0);
+      dst[4 * q] = v.x;
+      dst[4 * q + 1] = v.y;
+      dst[4 * q + 2] = v.z;
+      dst[4 * q + 3] = v.w;
+    }
+  } else if constexpr (N == 2) {
+    const f32x2 v = rbuf_ld2(r, voff, 0, 0);
+    dst[0] = v.x;
+    dst[1] = v.y;
   } else {
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-      if (p0 + j < U) st_vec<4>(es + 4 * (p0 + j), v + 4 * j);
-  }
-  if constexpr (OBS) {
-    float o[2 * K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      o[2 * j] = O.m[j];
-      o[2 * j + 1] = __builtin_bit_cast(float, O.e[j]);
-    }
-    if constexpr (VEC) {
-      if (p0 < U) st_vec<2 * K>(ob + 2 * p0, o);
-    } else {
-#pragma unroll
-      for (int j = 0; j < K; ++j)
-        if (p0 + j < U) st_vec<2>(ob + 2 * (p0 + j), o + 2 * j);
-    }
+    dst[0] = rbuf_ld1(r, voff, 0, 0);
   }
 }
-
-template <int K, bool OBS, bool VEC>
-__device__ __forceinline__ void slot_read(const float* es, const float* ob, XRow<K>& E,
-                                          XRow<K>& Sh, XRow<K>& O, int U, int lane) {
-  const int p0 = K * lane;
-  float v[4 * K];
-  if constexpr (VEC) {
-    if (p0 < U) {
-      ld_vec<4 * K>(v, es + 4 * p0);
-    } else {
+// N floats to byte offset voff
+template <int N>
+__device__ __forceinline__ void buf_st(const float* v, __amdgpu_buffer_rsrc_t r, int voff) {
+  if constexpr (N % 4 == 0) {
 #pragma unroll
-      for (int j = 0; j < 4 * K; ++j) v[j] = (j & 1) ? __builtin_bit_cast(float, XF_EZERO) : 0.0f;
-    }
+    for (int q = 0; q < N / 4; ++q)
+      rbuf_st4(f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]}, r, voff + 16 * q, 0, 0);
+  } else if constexpr (N == 2) {
+    rbuf_st2(f32x2{v[0], v[1]}, r, voff, 0, 0);
   } else {
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      if (p0 + j < U) {
-        ld_vec<4>(v + 4 * j, es + 4 * (p0 + j));
-      } else {
-        v[4 * j] = 0.0f;
-        v[4 * j + 1] = __builtin_bit_cast(float, XF_EZERO);
-        v[4 * j + 2] = 0.0f;
-        v[4 * j + 3] = __builtin_bit_cast(float, XF_EZERO);
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    E.m[j] = v[4 * j];
-    E.e[j] = __builtin_bit_cast(int, v[4 * j + 1]);
-    Sh.m[j] = v[4 * j + 2];
-    Sh.e[j] = __builtin_bit_cast(int, v[4 * j + 3]);
-  }
-  if constexpr (OBS) {
-    float o[2 * K];
-    if constexpr (VEC) {
-      if (p0 < U) {
-        ld_vec<2 * K>(o, ob + 2 * p0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          o[2 * j] = 0.0f;
-          o[2 * j + 1] = __builtin_bit_cast(float, XF_EZERO);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        if (p0 + j < U) {
-          ld_vec<2>(o + 2 * j, ob + 2 * (p0 + j));
-        } else {
-          o[2 * j] = 0.0f;
-          o[2 * j + 1] = __builtin_bit_cast(float, XF_EZERO);
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      O.m[j] = o[2 * j];
-      O.e[j] = __builtin_bit_cast(int, o[2 * j + 1]);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      O.m[j] = 1.0f;
-      O.e[j] = 0;
-    }
+    rbuf_st1(v[0], r, voff, 0, 0);
   }
 }
 
 template <int K>
+__device__ __forceinline__ void xrow_pack(const XRow<K>& r, float* v) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    v[2 * j] = r.m[j];
+    v[2 * j + 1] = __builtin_bit_cast(float, r.e[j]);
+  }
+}
+template <int K>
+__device__ __forceinline__ XRow<K> xrow_unpack(const float* v) {
+  XRow<K> r;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    r.m[j] = v[2 * j];
+    r.e[j] = __builtin_bit_cast(int, v[2 * j + 1]);
+  }
+  return r;
+}
+
+// Lattice-row storage (alpha rows of phase 1, beta rows of phase 1): LDS with junk/zero
+// redirection for lanes past U, or a global workspace through range-checked buffer ops.
+template <int K, bool LDS>
+struct RowStore {
+  xf* rows;        // LDS rows (LDS) or this utterance's workspace rows (global)
+  xf* junk;        // LDS: 64*K xf scratch for stores of lanes past U
+  const xf* zero;  // LDS: 64*K canonical zeros for loads of lanes past U
+  int U, lane;
+  bool act;
+  __device__ __forceinline__ void store(int s, const XRow<K>& r) const {
+    float v[2 * K];
+    xrow_pack<K>(r, v);
+    if constexpr (LDS) {
+      xf* p = act ? rows + (size_t)s * U + K * lane : junk + K * lane;
+      st_vec<2 * K>(reinterpret_cast<float*>(p), v);
+    } else {
+      buf_st<2 * K>(v, brsrc(rows + (size_t)s * U, (unsigned)U * 8u), K * lane * 8);
+    }
+  }
+  __device__ __forceinline__ XRow<K> load(int s) const {
+    float v[2 * K];
+    if constexpr (LDS) {
+      const xf* p = act ? rows + (size_t)s * U + K * lane : zero + K * lane;
+      ld_vec<2 * K>(v, reinterpret_cast<const float*>(p));
+    } else {
+      buf_ld<2 * K>(v, brsrc(rows + (size_t)s * U, (unsigned)U * 8u), K * lane * 8);
+#pragma unroll
+      for (int j = 0; j < K; ++j)  // out-of-range lanes read 0 bits: make them canonical zeros
+        if (!act) v[2 * j + 1] = __builtin_bit_cast(float, XF_EZERO);
+    }
+    return xrow_unpack<K>(v);
+  }
+};
+
+template <int K>
 constexpr int conv_depth() { return K <= 2 ? 8 : (K <= 4 ? 4 : 2); }
 
-template <int K, bool OBS, bool LDS, bool VEC, int NC, int R>
-__global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a) {
+// ISO: two extra idle waves at indices 4, 5 so that (with the usual round-robin wave -> SIMD
+// placement) the chain waves 0, 1 own SIMD 0, 1 and the converters share SIMD 2, 3.
+template <int K, bool OBS, bool LDS, int NC, int R, bool ISO>
+__global__ __launch_bounds__(64 * (2 + 2 * NC + (ISO ? 2 : 0))) void k_fwd_bwd_pipe(FwdBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR rsrcs
   const int lane = threadIdx.x & 63;
   const int T = a.T, U = a.U;
   const int S = a.step_len[b];
   const int P = a.pos_len[b];
   const bool term = (a.flags & SSNT_FLAG_TERMINAL_EMIT) != 0;
   const size_t TU = (size_t)T * U;
-  const float* __restrict__ lt = a.log_trans + (size_t)b * TU * 2;
-  const float* __restrict__ lo = OBS ? a.log_obs + (size_t)b * TU : nullptr;
-  float* __restrict__ g = a.grad ? a.grad + (size_t)b * TU * 2 : nullptr;
-  float* __restrict__ go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
-  float* __restrict__ la = a.log_alpha ? a.log_alpha + (size_t)b * TU : nullptr;
-  float* __restrict__ lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
+  const float* lt = a.log_trans + (size_t)b * TU * 2;
+  const float* lo = OBS ? a.log_obs + (size_t)b * TU : nullptr;
+  float* g = a.grad ? a.grad + (size_t)b * TU * 2 : nullptr;
+  float* go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
+  float* la = a.log_alpha ? a.log_alpha + (size_t)b * TU : nullptr;
+  float* lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
+  const int p0 = K * lane;
+  const bool act = p0 < U;
 
-  // LDS: control | cut buffer (64K xf) | rings [dir][R][slot] | storage rows (LDS mode)
+  // LDS: control | cut buffer (64K xf) | zero area (64K xf) | junk area (64K xf) |
+  //      rings [dir][R][E/S U*16 B + obs U*8 B] | storage rows (LDS mode)
   PipeCtl* ctl = reinterpret_cast<PipeCtl*>(smem);
   xf* cutb = reinterpret_cast<xf*>(smem + sizeof(PipeCtl));
-  const int es_words = ((U * 4 + 3) / 4) * 4;             // floats per E/S slot
-  const int ob_words = OBS ? ((U * 2 + 3) / 4) * 4 : 0;   // floats per obs slot
-  const int slot_words = es_words + ob_words;
-  float* rings = reinterpret_cast<float*>(cutb + 64 * K);
-  xf* rows = LDS ? reinterpret_cast<xf*>(rings + 2 * R * slot_words)
-                 : reinterpret_cast<xf*>(a.workspace) + (size_t)b * TU;
+  xf* zero = cutb + 64 * K;
+  xf* junk = zero + 64 * K;
+  const int es_words = U * 4;                // floats per E/S slot (U % K == 0 -> 16 B aligned)
+  const int ob_words = OBS ? U * 2 : 0;      // floats per obs slot
+  const int slot_words = es_words + ((ob_words + 3) & ~3);
+  float* rings = reinterpret_cast<float*>(junk + 64 * K);
+  xf* rows_base = LDS ? reinterpret_cast<xf*>(rings + 2 * R * slot_words)
+                      : reinterpret_cast<xf*>(a.workspace) + (size_t)b * TU;
+  const RowStore<K, LDS> store{rows_base, junk, zero, U, lane, act};
 
   const bool feasible = S >= 1 && P >= 1 && S <= T && P <= U && S >= P;
-  const int nw = 2 + 2 * NC;
+  const int nw = 2 + 2 * NC + (ISO ? 2 : 0);
   auto fill_rows = [&](int from, int w0, int wstep) {  // zero grads / -inf debug rows
-    for (int s = from + w0; s < T; s += wstep) {
-      float z[K], ninf[K];
+    float z[2 * K], ninf[K];
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        z[j] = 0.0f;
-        ninf[j] = -__builtin_inff();
-      }
-      if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, z, z, U, lane);
-      if (go) store_f_row<K, VEC>(go + (size_t)s * U, z, U, lane);
-      if (la) store_f_row<K, VEC>(la + (size_t)s * U, ninf, U, lane);
-      if (lb) store_f_row<K, VEC>(lb + (size_t)s * U, ninf, U, lane);
+    for (int j = 0; j < 2 * K; ++j) z[j] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < K; ++j) ninf[j] = -__builtin_inff();
+    for (int s = from + w0; s < T; s += wstep) {
+      if (g) buf_st<2 * K>(z, brsrc(g + (size_t)s * U * 2, U * 8u), p0 * 8);
+      if (go) buf_st<K>(z, brsrc(go + (size_t)s * U, U * 4u), p0 * 4);
+      if (la) buf_st<K>(ninf, brsrc(la + (size_t)s * U, U * 4u), p0 * 4);
+      if (lb) buf_st<K>(ninf, brsrc(lb + (size_t)s * U, U * 4u), p0 * 4);
     }
+  };
+  auto log_row = [&](float* dst, int s, const XRow<K>& r) {  // debug outputs (slow path)
+    float v[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = xf_log(xf{r.m[j], r.e[j]});
+    buf_st<K>(v, brsrc(dst + (size_t)s * U, U * 4u), p0 * 4);
   };
   const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
   if (!feasible) {
@@ -814,23 +832,33 @@ __global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a
     return;
   }
   if (threadIdx.x < 32) reinterpret_cast<int*>(ctl)[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < 64 * K; i += 64 * nw) zero[i] = xf_zero();
   __syncthreads();
   const int M = (S - 1) >> 1;
 
+  if (ISO && (wave == 4 || wave == 5)) return;
   if (wave >= 2) {
     // ------------------------------ converter -----------------------------------------
-    const int d = (wave - 2) / NC;  // 0 = forward stream, 1 = backward stream
-    const int c = (wave - 2) % NC;
+    const int ci = (ISO && wave > 5) ? wave - 4 : wave - 2;
+    const int d = ci / NC;  // 0 = forward stream, 1 = backward stream
+    const int c = ci % NC;
     constexpr int D = conv_depth<K>();
     float* ring_d = rings + (size_t)d * R * slot_words;
-    auto srow = [&](int r) { return d == 0 ? r : S - 1 - r; };
+    auto srow = [&](int r) { return min(max(d == 0 ? r : S - 1 - r, 0), T - 1); };
+    auto load = [&](int r, Item<K, OBS>& it) {
+      const int row = srow(r);
+      buf_ld<2 * K>(it.lt, brsrc(lt + (size_t)row * U * 2, U * 8u), p0 * 8);
+      if constexpr (OBS) {
+        const int orow = min(row + 1, T - 1);
+        buf_ld<K>(it.ob, brsrc(lo + (size_t)orow * U, U * 4u), p0 * 4);
+      }
+    };
     Item<K, OBS> pf[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-      const int row = srow(c + NC * i);
-      pf[i] = load_item<K, OBS, VEC>(lt, lo, row, row + 1, T, U, lane);
-    }
+    for (int i = 0; i < D; ++i) load(c + NC * i, pf[i]);
     int kseen = 0;
+    unsigned long long cg_wait = 0, cg_n = 0;
+    const unsigned long long cg_t0 = DIAG_T();
     const int nmine = (S - c + NC - 1) / NC;  // my stream rows: c, c+NC, ...
     for (int base = 0; base < nmine; base += D) {
 #pragma unroll
@@ -839,20 +867,47 @@ __global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a
         if (k < nmine) {
           const int r = c + NC * k;
           const Item<K, OBS> it = pf[i];
-          const int nrow = srow(r + NC * D);
-          pf[i] = load_item<K, OBS, VEC>(lt, lo, nrow, nrow + 1, T, U, lane);
+          load(r + NC * D, pf[i]);
           XRow<K> E, Sh, O;
           convert<K, OBS>(it, P, lane, E, Sh);
           convert_obs<K, OBS>(it, P, lane, O);
-          if (r - R >= kseen) kseen = spin_geq(&ctl->kprog[d], r - R + 1, a.status);
+          if (r - R >= kseen) {
+            const unsigned long long t = DIAG_T();
+            kseen = spin_geq(&ctl->kprog[d], r - R + 1, a.status);
+            cg_wait += DIAG_T() - t;
+            ++cg_n;
+          }
           float* slot = ring_d + (size_t)(r % R) * slot_words;
-          slot_write<K, OBS, VEC>(slot, slot + es_words, E, Sh, O, U, lane);
-          if (lane == 0) lds_release(&ctl->done[d][c], k + 1);
+          float v[4 * K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            v[4 * j] = E.m[j];
+            v[4 * j + 1] = __builtin_bit_cast(float, E.e[j]);
+            v[4 * j + 2] = Sh.m[j];
+            v[4 * j + 3] = __builtin_bit_cast(float, Sh.e[j]);
+          }
+          st_vec<4 * K>(act ? slot + 4 * p0 : reinterpret_cast<float*>(junk), v);
+          if constexpr (OBS) {
+            float o[2 * K];
+            xrow_pack<K>(O, o);
+            st_vec<2 * K>(act ? slot + es_words + 2 * p0 : reinterpret_cast<float*>(junk), o);
+          }
+          lds_release(&ctl->done[d][c], k + 1);
         }
       }
     }
-    // idle converters fill the rows beyond S
-    fill_rows(S, wave - 2, 2 * NC);
+#ifdef SSNT_DIAG
+    if (c == 0 && lane == 0) {
+      unsigned long long* dg = g_diag[b * 4 + 2 + d];
+      dg[0] = DIAG_T() - cg_t0;
+      dg[1] = cg_wait;
+      dg[2] = cg_n;
+      dg[5] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));  // HW_ID
+    }
+#else
+    (void)cg_wait; (void)cg_n; (void)cg_t0;
+#endif
+    fill_rows(S, ci, 2 * NC);  // idle converters zero the rows beyond S
     return;
   }
 
@@ -861,15 +916,22 @@ __global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a
   const bool fwd = (wave == 0);
   const int d = fwd ? 0 : 1;
   const float* ring_d = rings + (size_t)d * R * slot_words;
+  unsigned long long dg_wait = 0, dg_n = 0, dg_cut = 0, dg_p1 = 0;
+  const unsigned long long dg_t0 = DIAG_T();
   int ready = 0;  // stream rows known converted
   auto wait_row = [&](int r) {
     if (r < ready) return;
     int mn = 0x7fffffff;
     for (int c = 0; c < NC; ++c) {
-      // converter c has produced rows c, c+NC, ..., c+NC*(done-1): first missing c+NC*done
-      const int need = (r - c + NC) / NC;  // rows of c that must be done to cover r
+      // converter c produced rows c, c+NC, ..., c+NC*(done-1): its first missing row c+NC*done
+      const int need = (r - c + NC) / NC;
       int dn = lds_acquire(&ctl->done[d][c]);
-      if (c + NC * dn <= r && need > 0) dn = spin_geq(&ctl->done[d][c], need, a.status);
+      if (c + NC * dn <= r && need > 0) {
+        const unsigned long long t = DIAG_T();
+        dn = spin_geq<false>(&ctl->done[d][c], need, a.status);
+        dg_wait += DIAG_T() - t;
+        ++dg_n;
+      }
       mn = min(mn, c + NC * dn);
     }
     ready = mn;
@@ -877,13 +939,48 @@ __global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a
   auto read_row = [&](int r, XRow<K>& E, XRow<K>& Sh, XRow<K>& O) {
     wait_row(r);
     const float* slot = ring_d + (size_t)(r % R) * slot_words;
-    slot_read<K, OBS, VEC>(slot, slot + es_words, E, Sh, O, U, lane);
+    float v[4 * K];
+    ld_vec<4 * K>(v, act ? slot + 4 * p0 : reinterpret_cast<const float*>(zero));
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      E.m[j] = v[4 * j];
+      E.e[j] = act ? __builtin_bit_cast(int, v[4 * j + 1]) : XF_EZERO;
+      Sh.m[j] = v[4 * j + 2];
+      Sh.e[j] = act ? __builtin_bit_cast(int, v[4 * j + 3]) : XF_EZERO;
+    }
+    if constexpr (OBS) {
+      float o[2 * K];
+      ld_vec<2 * K>(o, act ? slot + es_words + 2 * p0 : reinterpret_cast<const float*>(zero));
+      O = xrow_unpack<K>(o);
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        O.m[j] = 1.0f;
+        O.e[j] = 0;
+      }
+    }
   };
-  auto consumed = [&](int r) {  // slot of stream row r may be reused (its reads are done)
-    if (lane == 0) lds_release(&ctl->kprog[d], r + 1);
+  // slot of stream row r may be reused: the stored value data-depends on row r's slot contents
+  // (x * 0.0f cannot be folded under IEEE), so the store issues only after those reads returned
+  auto consumed = [&](int r, const XRow<K>& E) {
+    lds_relaxed(&ctl->kprog[d], r + 1 + (int)(E.m[0] * 0.0f));
+  };
+  auto grad_row = [&](int s, const float* ge, const float* gs) {
+    float v[2 * K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      v[2 * j] = ge[j];
+      v[2 * j + 1] = gs[j];
+    }
+    buf_st<2 * K>(v, brsrc(g + (size_t)s * U * 2, U * 8u), p0 * 8);
+  };
+  auto bail = [&]() {  // Z == 0: release the converters, zero everything (chains only)
+    lds_relaxed(&ctl->kprog[d], 0x3fffffff);
+    fill_rows(0, wave, 2);
+    if (threadIdx.x == 0) a.loss[b] = inf_loss;
   };
 
-  XRow<K> X;
+  XRow<K> X, E, Sh, O;
   if (fwd) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -901,51 +998,28 @@ __global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a
         X.e[0] = 1;
       }
     }
-    store_row<K, VEC>(rows, X, U, lane);
-    if (la) store_log_row<K, VEC>(la, X, U, lane);
-    // phase 1: alpha[1..M]
+    store.store(0, X);
+    if (la) log_row(la, 0, X);
+    read_row(0, E, Sh, O);
+    // ---- phase 1: alpha[1..M] ----
     for (int r = 0; r < M; ++r) {
-      XRow<K> E, Sh, O, stay, shft;
-      read_row(r, E, Sh, O);
+      consumed(r, E);
+      XRow<K> En, Shn, On, stay, shft;
+      read_row(r + 1, En, Shn, On);  // one step ahead, off the serial chain
       alpha_step<K, OBS>(X, E, Sh, O, stay, shft);
-      consumed(r);
-      store_row<K, VEC>(rows + (size_t)(r + 1) * U, X, U, lane);
-      if (la) store_log_row<K, VEC>(la + (size_t)(r + 1) * U, X, U, lane);
+      store.store(r + 1, X);
+      if (la) log_row(la, r + 1, X);
+      E = En;
+      Sh = Shn;
+      O = On;
     }
-  } else {
-    // init from stream row 0 (= row S-1): terminal emit
+    dg_p1 = DIAG_T() - dg_t0;
+    // ---- cut: Z = tree-sum over p of alpha[M][p] * beta[M][p] ----
     {
-      XRow<K> E, Sh, O;
-      read_row(0, E, Sh, O);
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const bool last = (K * lane + j) == P - 1;
-        xf v = term ? xf_norm(E.m[j], E.e[j]) : xf{0.5f, 1};
-        X.m[j] = last ? v.m : 0.0f;
-        X.e[j] = last ? v.e : XF_EZERO;
-      }
-      consumed(0);
-      const int s = S - 1;
-      if (s > M) store_row<K, VEC>(rows + (size_t)s * U, X, U, lane);
-      else store_row<K, VEC>(cutb, X, 64 * K, lane);
-      if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
+      const unsigned long long t = DIAG_T();
+      spin_geq(&ctl->bm_ready, 1, a.status);
+      dg_cut += DIAG_T() - t;
     }
-    for (int r = 1; r < S - M; ++r) {  // beta[S-2..M]
-      const int s = S - 1 - r;
-      XRow<K> E, Sh, O, Q, R_;
-      read_row(r, E, Sh, O);
-      entering<K, OBS>(X, O, Q, R_);
-      beta_step<K>(X, E, Sh, Q, R_);
-      consumed(r);
-      if (s > M) store_row<K, VEC>(rows + (size_t)s * U, X, U, lane);
-      else store_row<K, VEC>(cutb, X, 64 * K, lane);
-      if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
-    }
-    if (lane == 0) lds_release(&ctl->bm_ready, 1);
-  }
-  // ------------------------------ cut ----------------------------------------------------
-  if (fwd) {
-    spin_geq(&ctl->bm_ready, 1, a.status);
     float wm[K];
     int we[K];
 #pragma unroll
@@ -958,9 +1032,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a
     for (int len = K; len > 1; len >>= 1) {
 #pragma unroll
       for (int i = 0; i < len / 2; ++i) {
-        const xf r = xf_add(wm[2 * i], we[2 * i], wm[2 * i + 1], we[2 * i + 1]);
-        wm[i] = r.m;
-        we[i] = r.e;
+        const xf t = xf_add(wm[2 * i], we[2 * i], wm[2 * i + 1], we[2 * i + 1]);
+        wm[i] = t.m;
+        we[i] = t.e;
       }
     }
     xf z{wm[0], we[0]};
@@ -970,92 +1044,161 @@ __global__ __launch_bounds__(64 * (2 + 2 * NC)) void k_fwd_bwd_pipe(FwdBwdArgs a
       const int oe = __shfl_xor(z.e, off);
       z = xf_add(z.m, z.e, om, oe);
     }
-    if (lane == 0) {
-      ctl->z = z;
-      lds_release(&ctl->z_ready, 1);
+    if (lane == 0) ctl->z = z;
+    lds_release(&ctl->z_ready, 1);
+    if (z.m == 0.0f) {
+      bail();
+      return;
     }
-  } else {
-    spin_geq(&ctl->z_ready, 1, a.status);
-  }
-  const xf Z = ctl->z;
-  if (Z.m == 0.0f) {  // numerically infeasible: release the converters, zero everything
-    if (lane == 0) lds_relaxed(&ctl->kprog[d], 0x3fffffff);
-    fill_rows(0, wave, 2);
-    if (threadIdx.x == 0) a.loss[b] = inf_loss;
-    return;
-  }
-  if (fwd && lane == 0) a.loss[b] = 0.0f - xf_log(Z);
-  const float izm = 1.0f / Z.m;
-  const int ize = -Z.e;
-  // ------------------------------ phase 2 ------------------------------------------------
-  if (fwd) {
-    for (int s = M; s < S; ++s) {  // transition s: alpha[s] (X) -> row s+1
-      XRow<K> E, Sh, O, Q, R_;
-      read_row(s, E, Sh, O);
-      if (s + 1 < S) {
-        const XRow<K> Bn = load_row<K, VEC>(rows + (size_t)(s + 1) * U, U, lane);
+    if (lane == 0) a.loss[b] = 0.0f - xf_log(z);
+    const float izm = 1.0f / z.m;
+    const int ize = -z.e;
+    // ---- phase 2: transitions M..S-1 ----
+    XRow<K> Bn = M + 1 < S ? store.load(M + 1) : XRow<K>{};
+    for (int s = M; s < S; ++s) {
+      consumed(s, E);
+      const bool more = s + 1 < S;
+      XRow<K> En, Shn, On, Bnn;
+      if (more) read_row(s + 1, En, Shn, On);
+      if (s + 2 < S) Bnn = store.load(s + 2);
+      XRow<K> Q, R_;
+      if (more) {
         entering<K, OBS>(Bn, O, Q, R_);
       } else {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          const bool last = term && (K * lane + j) == P - 1;
+          const bool last = term && (p0 + j) == P - 1;
           Q.m[j] = last ? 1.0f : 0.0f;
           Q.e[j] = last ? 0 : XF_EZERO;
           R_.m[j] = 0.0f;
           R_.e[j] = XF_EZERO;
         }
       }
-      float ge[K], gs[K];
       if constexpr (OBS) {
-        const XRow<K> Bs = (s == M) ? load_row<K, VEC>(cutb, 64 * K, lane)
-                                    : load_row<K, VEC>(rows + (size_t)s * U, U, lane);
+        const XRow<K> Bs = (s == M) ? xrow_unpack<K>(reinterpret_cast<const float*>(cutb + p0))
+                                    : store.load(s);
         float gob[K];
 #pragma unroll
         for (int j = 0; j < K; ++j)
           gob[j] = xf_neg_post((X.m[j] * Bs.m[j]) * izm, X.e[j] + Bs.e[j] + ize);
-        if (go) store_f_row<K, VEC>(go + (size_t)s * U, gob, U, lane);
+        if (go) buf_st<K>(gob, brsrc(go + (size_t)s * U, U * 4u), p0 * 4);
       }
       XRow<K> stay, shft;
       XRow<K> Xn = X;
       alpha_step<K, OBS>(Xn, E, Sh, O, stay, shft);
-      consumed(s);
+      float ge[K], gs[K];
 #pragma unroll
       for (int j = 0; j < K; ++j) {
         ge[j] = xf_neg_post((stay.m[j] * Q.m[j]) * izm, stay.e[j] + Q.e[j] + ize);
         gs[j] = xf_neg_post((shft.m[j] * R_.m[j]) * izm, shft.e[j] + R_.e[j] + ize);
       }
-      if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, ge, gs, U, lane);
-      if (s + 1 < S) {
+      if (g) grad_row(s, ge, gs);
+      if (more) {
         X = Xn;
-        if (la) store_log_row<K, VEC>(la + (size_t)(s + 1) * U, X, U, lane);
+        if (la) log_row(la, s + 1, X);
+        E = En;
+        Sh = Shn;
+        O = On;
+        Bn = Bnn;
       }
     }
   } else {
-    for (int r = S - M; r < S; ++r) {  // transition s = S-1-r: beta[s+1] (X) -> beta[s]
+    // ---- backward chain: stream row r is lattice row S-1-r ----
+    read_row(0, E, Sh, O);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {  // terminal emit (src/lib.rs:187-195)
+      const bool last = (p0 + j) == P - 1;
+      xf v = term ? xf_norm(E.m[j], E.e[j]) : xf{0.5f, 1};
+      X.m[j] = last ? v.m : 0.0f;
+      X.e[j] = last ? v.e : XF_EZERO;
+    }
+    auto put_beta = [&](int s) {
+      if (s > M) {
+        store.store(s, X);
+      } else {
+        float v[2 * K];
+        xrow_pack<K>(X, v);
+        st_vec<2 * K>(reinterpret_cast<float*>(cutb + p0), v);
+        lds_release(&ctl->bm_ready, 1);
+      }
+      if (lb) log_row(lb, s, X);
+    };
+    put_beta(S - 1);
+    consumed(0, E);
+    if (S > 1) read_row(1, E, Sh, O);
+    // ---- phase 1: beta[S-2..M] ----
+    for (int r = 1; r < S - M; ++r) {
+      consumed(r, E);
       const int s = S - 1 - r;
-      XRow<K> E, Sh, O, Q, R_;
-      read_row(r, E, Sh, O);
+      XRow<K> En, Shn, On, Q, R_;
+      if (r + 1 < S) read_row(r + 1, En, Shn, On);
       entering<K, OBS>(X, O, Q, R_);
-      const XRow<K> A = load_row<K, VEC>(rows + (size_t)s * U, U, lane);
-      float ge[K], gs[K];
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        ge[j] = xf_neg_post(((A.m[j] * E.m[j]) * Q.m[j]) * izm, A.e[j] + E.e[j] + Q.e[j] + ize);
-        gs[j] = xf_neg_post(((A.m[j] * Sh.m[j]) * R_.m[j]) * izm, A.e[j] + Sh.e[j] + R_.e[j] + ize);
-      }
       beta_step<K>(X, E, Sh, Q, R_);
-      consumed(r);
-      if constexpr (OBS) {
-        float gob[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-          gob[j] = xf_neg_post((A.m[j] * X.m[j]) * izm, A.e[j] + X.e[j] + ize);
-        if (go) store_f_row<K, VEC>(go + (size_t)s * U, gob, U, lane);
+      put_beta(s);
+      E = En;
+      Sh = Shn;
+      O = On;
+    }
+    dg_p1 = DIAG_T() - dg_t0;
+    if (M > 0) {
+      // ---- phase 2: transitions M-1..0 ----
+      {
+        const unsigned long long t = DIAG_T();
+        spin_geq(&ctl->z_ready, 1, a.status);
+        dg_cut += DIAG_T() - t;
       }
-      if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, ge, gs, U, lane);
-      if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
+      const xf z = ctl->z;
+      if (z.m == 0.0f) {
+        bail();
+        return;
+      }
+      const float izm = 1.0f / z.m;
+      const int ize = -z.e;
+      XRow<K> A = store.load(M - 1);
+      for (int r = S - M; r < S; ++r) {  // transition s = S-1-r
+        consumed(r, E);
+        const int s = S - 1 - r;
+        XRow<K> En, Shn, On, An;
+        if (r + 1 < S) read_row(r + 1, En, Shn, On);
+        if (s > 0) An = store.load(s - 1);
+        XRow<K> Q, R_;
+        entering<K, OBS>(X, O, Q, R_);
+        float ge[K], gs[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          ge[j] = xf_neg_post(((A.m[j] * E.m[j]) * Q.m[j]) * izm, A.e[j] + E.e[j] + Q.e[j] + ize);
+          gs[j] = xf_neg_post(((A.m[j] * Sh.m[j]) * R_.m[j]) * izm, A.e[j] + Sh.e[j] + R_.e[j] + ize);
+        }
+        beta_step<K>(X, E, Sh, Q, R_);
+        if constexpr (OBS) {
+          float gob[K];
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            gob[j] = xf_neg_post((A.m[j] * X.m[j]) * izm, A.e[j] + X.e[j] + ize);
+          if (go) buf_st<K>(gob, brsrc(go + (size_t)s * U, U * 4u), p0 * 4);
+        }
+        if (g) grad_row(s, ge, gs);
+        if (lb) log_row(lb, s, X);
+        E = En;
+        Sh = Shn;
+        O = On;
+        A = An;
+      }
     }
   }
+#ifdef SSNT_DIAG
+  if (lane == 0) {
+    unsigned long long* dg = g_diag[b * 4 + d];
+    dg[0] = DIAG_T() - dg_t0;
+    dg[1] = dg_wait;
+    dg[2] = dg_n;
+    dg[3] = dg_cut;
+    dg[4] = dg_p1;
+    dg[5] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));  // HW_ID
+  }
+#else
+  (void)dg_wait; (void)dg_n; (void)dg_cut; (void)dg_p1; (void)dg_t0;
+#endif
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -1092,17 +1235,16 @@ int launch_k(const FwdBwdArgs& a, hipStream_t st) {
   return vec ? launch_kernel<K, OBS, false, true>(a, shm, st) : launch_kernel<K, OBS, false, false>(a, shm, st);
 }
 
-constexpr int kPipeNC = 2;  // converter waves per direction
 constexpr int kPipeR = 8;   // ring slots per direction
 
 inline size_t pipe_head_bytes(int K, int U, bool obs) {
-  const size_t es = ((size_t)U * 4 + 3) / 4 * 4, ob = obs ? ((size_t)U * 2 + 3) / 4 * 4 : 0;
-  return sizeof(PipeCtl) + (size_t)64 * K * sizeof(xf) + 2 * (size_t)kPipeR * (es + ob) * 4;
+  const size_t slot_words = (size_t)U * 4 + ((obs ? (size_t)U * 2 : 0) + 3) / 4 * 4;
+  return sizeof(PipeCtl) + 3 * (size_t)64 * K * sizeof(xf) + 2 * (size_t)kPipeR * slot_words * 4;
 }
 
-template <int K, bool OBS, bool LDS, bool VEC>
+template <int K, bool OBS, bool LDS, int NC, bool ISO>
 int launch_pipe_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
-  auto kern = k_fwd_bwd_pipe<K, OBS, LDS, VEC, kPipeNC, kPipeR>;
+  auto kern = k_fwd_bwd_pipe<K, OBS, LDS, NC, kPipeR, ISO>;
   if (lds > 64 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
@@ -1111,30 +1253,29 @@ int launch_pipe_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
       attr_set = true;
     }
   }
-  hipLaunchKernelGGL(kern, dim3(a.B), dim3(64 * (2 + 2 * kPipeNC)), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(64 * (2 + 2 * NC + (ISO ? 2 : 0))), lds, st, a);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
-template <int K, bool OBS>
+template <int K, bool OBS, int NC, bool ISO = false>
 int launch_pipe(const FwdBwdArgs& a, hipStream_t st) {
+  const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
+                   aligned16(a.grad) && aligned16(a.grad_obs) && aligned16(a.log_alpha) &&
+                   aligned16(a.log_beta) && aligned16(a.workspace);
+  if (!vec) return launch_k<K, OBS>(a, st);  // odd shapes: the simple kernel
   const size_t head = pipe_head_bytes(K, a.U, OBS);
   const size_t rows = (size_t)a.T * a.U * sizeof(xf);
   if (head > kLdsBudget) return SSNT_ERR_UNSUPPORTED;
   const bool lds = head + rows <= kLdsBudget;
   if (!lds && (a.workspace == nullptr || a.workspace_bytes < (size_t)a.B * rows))
     return SSNT_ERR_WORKSPACE;
-  const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
-                   aligned16(a.grad) && aligned16(a.grad_obs) && aligned16(a.log_alpha) &&
-                   aligned16(a.log_beta) && aligned16(a.workspace);
-  const size_t shm = lds ? head + rows : head;
-  if (lds)
-    return vec ? launch_pipe_kernel<K, OBS, true, true>(a, shm, st)
-               : launch_pipe_kernel<K, OBS, true, false>(a, shm, st);
-  return vec ? launch_pipe_kernel<K, OBS, false, true>(a, shm, st)
-             : launch_pipe_kernel<K, OBS, false, false>(a, shm, st);
+  return lds ? launch_pipe_kernel<K, OBS, true, NC, ISO>(a, head + rows, st)
+             : launch_pipe_kernel<K, OBS, false, NC, ISO>(a, head, st);
 }
 
-int g_variant = -1;  // -1: not chosen yet (env SSNT_FWD_BWD_KERNEL), 0 pipelined, 1 simple
+// -1: not chosen yet (env SSNT_FWD_BWD_KERNEL), 0 pipelined (3 converters per direction),
+// 1 simple two-wave kernel, 2 pipelined with 2 converters per direction
+int g_variant = -1;
 
 inline bool use_simple_kernel() {
   if (g_variant < 0) {
@@ -1153,10 +1294,24 @@ int launch_obs(const FwdBwdArgs& a, hipStream_t st) {
     if (a.U <= 512) return launch_k<8, OBS>(a, st);
     return SSNT_ERR_UNSUPPORTED;
   }
-  if (a.U <= 64) return launch_pipe<1, OBS>(a, st);
-  if (a.U <= 128) return launch_pipe<2, OBS>(a, st);
-  if (a.U <= 256) return launch_pipe<4, OBS>(a, st);
-  if (a.U <= 512) return launch_pipe<8, OBS>(a, st);
+  if (g_variant == 3) {
+    if (a.U <= 64) return launch_pipe<1, OBS, 2, true>(a, st);
+    if (a.U <= 128) return launch_pipe<2, OBS, 2, true>(a, st);
+    if (a.U <= 256) return launch_pipe<4, OBS, 2, true>(a, st);
+    if (a.U <= 512) return launch_pipe<8, OBS, 2, true>(a, st);
+    return SSNT_ERR_UNSUPPORTED;
+  }
+  if (g_variant == 2) {
+    if (a.U <= 64) return launch_pipe<1, OBS, 2>(a, st);
+    if (a.U <= 128) return launch_pipe<2, OBS, 2>(a, st);
+    if (a.U <= 256) return launch_pipe<4, OBS, 2>(a, st);
+    if (a.U <= 512) return launch_pipe<8, OBS, 2>(a, st);
+    return SSNT_ERR_UNSUPPORTED;
+  }
+  if (a.U <= 64) return launch_pipe<1, OBS, 3>(a, st);
+  if (a.U <= 128) return launch_pipe<2, OBS, 3>(a, st);
+  if (a.U <= 256) return launch_pipe<4, OBS, 3>(a, st);
+  if (a.U <= 512) return launch_pipe<8, OBS, 3>(a, st);
   return SSNT_ERR_UNSUPPORTED;
 }
 
@@ -1172,8 +1327,20 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
   return (size_t)B * rows;
 }
 
+int diag_read(void* host, size_t bytes) {
+#ifdef SSNT_DIAG
+  if (bytes > sizeof(g_diag)) bytes = sizeof(g_diag);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? (int)bytes : -1;
+#else
+  (void)host;
+  (void)bytes;
+  return -1;
+#endif
+}
+
 int set_fwd_bwd_variant(int v) {
-  if (v < 0 || v > 1) return SSNT_ERR_INVALID_ARG;
+  if (v < 0 || v > 3) return SSNT_ERR_INVALID_ARG;
   g_variant = v;
   return SSNT_OK;
 }

@@ -36,6 +36,7 @@ struct FwdBwdArgs {
 size_t fwd_bwd_workspace_bytes(int B, int T, int U);
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
 int set_fwd_bwd_variant(int v);
+int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only
 
 // ---- beam-search decode (decode.hip) ----
 enum class Variant : int { V1 = 0, V2 = 1, Tone = 2 };

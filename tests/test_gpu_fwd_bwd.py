@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 F_TERM, F_ZINF = 1, 2
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["pipelined", "simple"])
+@pytest.fixture(autouse=True, params=[0, 1, 2, 3], ids=["pipelined3", "simple", "pipelined2", "pipelined2iso"])
 def kernel_variant(request, gpu):
     """Every parity case runs on both kernel variants (they must be bit-identical)."""
     lib = gpu.load()

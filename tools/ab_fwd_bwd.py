@@ -14,7 +14,7 @@ sys.path.insert(0, str(ROOT / "ssnt-tts-rust_amd"))
 import ssnt_tts_amd as S  # noqa: E402
 
 
-def bench_shape(B, T, U, variants=(0, 1), rounds=5, iters=10):
+def bench_shape(B, T, U, variants=(0, 2, 3, 1), rounds=5, iters=10):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(0)
