@@ -14,12 +14,9 @@ ORACLE    := oracle/build/libssnt_oracle.so
 # the CPU oracle reproduces it bit for bit. Correctly rounded f32 division is HIP's default.
 HIPFLAGS  := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall \
              -Wno-unused-function -I include -I $(CSRC)
-HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/decode.hip $(CSRC)/capi.hip
+HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/fwd_bwd_stream.hip $(CSRC)/decode.hip $(CSRC)/capi.hip
 HIP_HDRS  := $(wildcard $(CSRC)/*.h) include/ssnt_tts_c.h
 HIP_OBJS  := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(HIP_SRCS))
-
-DIAGDIR   := $(LIBDIR)/diag
-DIAG_OBJS := $(patsubst $(CSRC)/%.hip,$(DIAGDIR)/obj/%.o,$(HIP_SRCS))
 
 all: lib oracle
 
@@ -33,13 +30,25 @@ $(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 $(LIB): $(HIP_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(HIP_OBJS) -Wl,-soname,libssnt_tts_c.so
 
-# diagnostic build with in-kernel s_memtime stamps (tools/diag_fwd_bwd.py); never the product
+# diagnostic build with in-kernel s_memtime totals (tools/diag_fwd_bwd.py); never the product
+DIAGDIR   := $(LIBDIR)/diag
+DIAG_OBJS := $(patsubst $(CSRC)/%.hip,$(DIAGDIR)/obj/%.o,$(HIP_SRCS))
 lib-diag: $(DIAGDIR)/libssnt_tts_c.so
 $(DIAGDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -DSSNT_DIAG -c $< -o $@
 $(DIAGDIR)/libssnt_tts_c.so: $(DIAG_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(DIAG_OBJS) -Wl,-soname,libssnt_tts_c.so
+
+# experiment build: one kernel instance (K=2, no log_obs), diag stamps, SSNT_EXP env knobs
+EXPDIR    := $(LIBDIR)/exp
+EXP_OBJS  := $(patsubst $(CSRC)/%.hip,$(EXPDIR)/obj/%.o,$(HIP_SRCS))
+lib-exp: $(EXPDIR)/libssnt_tts_c.so
+$(EXPDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DSSNT_DIAG -DSSNT_EXP -c $< -o $@
+$(EXPDIR)/libssnt_tts_c.so: $(EXP_OBJS)
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(EXP_OBJS) -Wl,-soname,libssnt_tts_c.so
 
 $(ORACLE): oracle/ssnt_oracle.c
 	@mkdir -p $(dir $@)
@@ -48,4 +57,4 @@ $(ORACLE): oracle/ssnt_oracle.c
 clean:
 	rm -rf $(LIBDIR) oracle/build
 
-.PHONY: all lib lib-diag oracle clean
+.PHONY: all lib lib-diag lib-exp oracle clean

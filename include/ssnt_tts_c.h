@@ -98,7 +98,8 @@ typedef enum {
   SSNT_ERR_UNSUPPORTED = 5,       /* size outside what the kernels handle */
   SSNT_ERR_WORKSPACE = 6,         /* workspace missing / too small */
   SSNT_ERR_BAD_LENGTH = 7,        /* a length exceeds the tensor extent */
-  SSNT_ERR_BAD_INDEX = 8          /* backtrace branch index outside [0, W) */
+  SSNT_ERR_BAD_INDEX = 8,         /* backtrace branch index outside [0, W) */
+  SSNT_ERR_INTERNAL = 9           /* fwd-bwd: a bounded intra-kernel wait expired (a bug) */
 } ssnt_status;
 
 const char *ssnt_status_string(int status);
@@ -122,10 +123,10 @@ int ssnt_version(char *buf, size_t len);
  * default); `workspace` must hold ssnt_fwd_bwd_workspace_size() bytes (may be 0 -> NULL);
  * `status` (device int, may be NULL) receives error bits. Asynchronous. */
 size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos);
-/* Kernel variant for the forward-backward (results are bit-identical): 0 = pipelined, three
- * converter waves per direction feed two chain waves through LDS rings (default); 1 = simple
- * two-wave kernel; 2 = pipelined with two converters per direction. Process-wide; env
- * SSNT_FWD_BWD_KERNEL=simple selects 1 at first use. For A/B timing and debugging. */
+/* Kernel variant for the forward-backward (results are bit-identical): 0 = streaming kernel
+ * (two chain waves fed by converter waves, gradient waves behind them; default; shapes it does
+ * not take fall back to 1); 1 = two-wave kernel. Process-wide; env SSNT_FWD_BWD_KERNEL=simple
+ * selects 1 at first use. For A/B timing and debugging. */
 int ssnt_fwd_bwd_set_variant(int variant);
 int ssnt_fwd_bwd_device(const float *log_trans, const float *log_obs, const int *step_len,
                         const int *pos_len, int batch, int max_steps, int max_pos, int flags,

@@ -23,6 +23,7 @@ int status_bits_to_code(int bits) {
   if (bits & kStatusDurationMismatch) return SSNT_ERR_DURATION_MISMATCH;
   if (bits & kStatusBadLength) return SSNT_ERR_BAD_LENGTH;
   if (bits & kStatusBadIndex) return SSNT_ERR_BAD_INDEX;
+  if (bits & kStatusTimeout) return SSNT_ERR_INTERNAL;
   return SSNT_OK;
 }
 
@@ -223,6 +224,7 @@ const char* ssnt_status_string(int status) {
     case SSNT_ERR_WORKSPACE: return "workspace missing or too small";
     case SSNT_ERR_BAD_LENGTH: return "length exceeds tensor extent";
     case SSNT_ERR_BAD_INDEX: return "beam branch index out of range";
+    case SSNT_ERR_INTERNAL: return "internal: a bounded intra-kernel wait expired";
     default: return "unknown status";
   }
 }
@@ -456,6 +458,7 @@ int ssnt_fwd_bwd_set_variant(int variant) { return set_fwd_bwd_variant(variant);
 
 // diagnostic builds (make lib-diag) only; not part of the public header
 int ssnt_diag_read(void* host, size_t bytes) { return diag_read(host, bytes); }
+
 
 size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos) {
   if (batch <= 0 || max_steps <= 0 || max_pos <= 0) return 0;

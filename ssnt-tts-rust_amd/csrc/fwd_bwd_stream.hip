@@ -1,0 +1,885 @@
+// fwd_bwd_stream.hip -- streaming lattice forward-backward for gfx950 (the default kernel).
+//
+// Same lattice and the same split-exponent arithmetic as the two-wave kernel in fwd_bwd.hip
+// (DESIGN.md "Lattice semantics", "Split-exponent arithmetic"); bit-exact with
+// oracle/ssnt_oracle.c. What differs is who does what. One workgroup = one utterance, ten waves:
+//
+//   wave 0      alpha chain: alpha[1..S-1], nothing else on its instruction stream
+//   wave 1      beta chain:  beta[S-1..0]
+//   waves 2..5  converters (2 per direction): load log_trans / log_obs rows from HBM, exp() them
+//               into split-exponent factors, write them to an R-slot LDS ring per direction.
+//               The forward ring holds the shift factors pre-shifted by one position
+//               (L[p] = Sh[p-1]), so the alpha chain's only cross-lane move is a DPP of its own
+//               row that the compiler folds into the multiply (v_mul_f32_dpp / v_add_u32_dpp).
+//   waves 6..9  gradient waves (2 per direction): one of them forms Z at the cut M = (S-1)>>1,
+//               then they emit d loss / d log_trans (and d loss / d log_obs) row by row behind
+//               the chains, reading the chain rows, the stored rows and the converted factors.
+//
+// The cost model that shapes this (measured, tools/micro/): a lone wave issues one VALU
+// instruction per ~4.4 cycles whether or not the instructions depend on each other, so a chain
+// step costs its instruction count. The chains therefore carry only the recurrence; every
+// other instruction lives on another wave.
+//
+// Rows kept for the gradients: alpha[0..M] and beta[M+1..S-1] in "storage" (LDS when T*U*8 B
+// fits beside the rings, else a global workspace), beta[M] in a cut buffer; the chain rows past
+// the cut (alpha[M+1..], beta[..M-1]) go through a 4-row LDS ring to the gradient waves.
+//
+// Synchronisation is all LDS counters in one workgroup. A wave's DS instructions execute in
+// order, so "write data, then store counter" publishes and "read slot, then store counter"
+// releases without a wait; a compiler barrier keeps the program order. Every spin is bounded
+// (status bit kStatusTimeout).
+//
+// Lanes past U (p0 = K*lane >= U) read a clamped valid position and write to a junk area; their
+// values never reach a valid position except multiplied by a masked (exact zero) factor.
+#include <hip/hip_runtime.h>
+#include <limits.h>
+
+#include <type_traits>
+
+#include "lattice_dev.h"
+
+namespace ssnt {
+namespace {
+
+constexpr int kMaxW = 4;  // max converter / gradient waves per direction
+constexpr int kSpinLimit = 1 << 22;
+constexpr size_t kCtlBytes = 256;
+
+template <bool OBS>
+constexpr int in_slots() { return OBS ? 4 : 8; }  // converted-row ring slots per direction
+template <bool OBS>
+constexpr int out_slots() { return OBS ? 4 : 8; }  // chain-row ring (rows past the cut) per direction
+template <int K>
+constexpr int conv_depth() { return K <= 2 ? 8 : (K <= 4 ? 4 : 2); }  // converter prefetch rows
+
+// experiment knobs (SSNT_EXP builds only; compiled out of the product)
+#ifdef SSNT_EXP
+#define EXP(bit) ((a.exp >> (bit)) & 1)
+#else
+#define EXP(bit) false
+#endif
+
+struct Ctl {
+  int conv[2][kMaxW];  // per direction / converter: rows of its share written to the ring
+  int chain[2];        // per direction: stream rows the chain has finished (outputs written)
+  int sread[2];        // per direction: stream rows whose ring slots the chain has read
+  int help[2][kMaxW];  // per direction / gradient wave: rows of its share finished
+  int a_ready;       // alpha[0..M] stored
+  int bm_ready;      // beta[M+1..S-1] stored, beta[M] in the cut buffer
+  int z_ready;       // Z published
+  int pad;
+  xf z;
+};
+static_assert(sizeof(Ctl) <= kCtlBytes, "control block");
+
+__device__ __forceinline__ int ctr_ld(const int* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ int ctr_acq(const int* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void ctr_st(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ctr_rel(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// compiler-only barrier: keeps LDS data accesses and counter accesses in program order (the
+// hardware then executes them in that order)
+__device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
+
+// Diagnostic build only (-DSSNT_DIAG, `make lib-diag`): per-wave s_memtime totals, read back
+// with ssnt_diag_read() (tools/diag_fwd_bwd.py). g_diag[b][wave][8]: 0 total cycles, 1 cycles
+// spent spinning, 2 spins that waited, 3 cycle of the cut (chains: alpha[M] / beta[M] stored;
+// gradient waves: Z known). Never present in the product build.
+#ifdef SSNT_DIAG
+__device__ unsigned long long g_diag[1024][2 + 4 * kMaxW][8];
+struct Diag {
+  unsigned long long t0 = __builtin_amdgcn_s_memtime(), wait = 0, cut = 0;
+  unsigned long long n = 0;
+  __device__ unsigned long long now() const { return __builtin_amdgcn_s_memtime(); }
+  __device__ void mark_cut() { cut = now() - t0; }
+  __device__ void flush(int b, int w) {
+    if ((threadIdx.x & 63) == 0 && b < 1024) {
+      g_diag[b][w][0] = now() - t0;
+      g_diag[b][w][1] = wait;
+      g_diag[b][w][2] = n;
+      g_diag[b][w][3] = cut;
+    }
+  }
+};
+#else
+struct Diag {
+  __device__ unsigned long long now() const { return 0; }
+  __device__ void mark_cut() {}
+  __device__ void flush(int, int) {}
+  unsigned long long wait = 0, n = 0;
+};
+#endif
+
+// spin until f() >= target (bounded); returns the last value seen
+template <bool SLEEP, typename F>
+__device__ __forceinline__ int spin_until(F f, int target, int* status, Diag& dg) {
+  int v = f();
+  if (v >= target) return v;
+  const unsigned long long t = dg.now();
+  ++dg.n;
+  for (int n = 0; v < target; ++n) {
+    if (n > kSpinLimit) {
+      if (status && (threadIdx.x & 63) == 0) atomicOr(status, kStatusTimeout);
+      return target;
+    }
+    if constexpr (SLEEP) __builtin_amdgcn_s_sleep(1);
+    v = f();
+  }
+  dg.wait += dg.now() - t;
+  return v;
+}
+
+// workers w = 0..NW-1 own rows begin + w + NW*i; counter w = rows done. First row not done.
+template <int NW>
+__device__ __forceinline__ int first_missing(const int* cnt, int begin) {
+  int m = INT_MAX;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) m = min(m, begin + w + NW * ctr_ld(cnt + w));
+  return m;
+}
+
+// neighbour moves with zero fill at the wave edge (bound_ctrl): foldable into the consumer
+__device__ __forceinline__ float shr_z(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ int shr_z(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x138, 0xf, 0xf, true); }
+__device__ __forceinline__ float shl_z(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x130, 0xf, 0xf, true));
+}
+__device__ __forceinline__ int shl_z(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x130, 0xf, 0xf, true); }
+
+// (ma,ea) + (mb,eb) -> normalized; zero results keep a (very negative) exponent >= XF_EZERO
+// instead of exactly XF_EZERO: the mantissa is the same as xf_add's and a zero's exponent stays
+// below every live exponent, so every value downstream is bit-identical.
+__device__ __forceinline__ void chain_add(float ma, int ea, float mb, int eb, float om, int oe,
+                                          bool obs, float& m, int& e) {
+  const int em = max(ea, eb);
+  float s = xldexp(ma, ea - em) + xldexp(mb, eb - em);
+  int ee = em;
+  if (obs) {
+    s = s * om;
+    ee = ee + oe;
+  }
+  m = xmant(s);
+  e = max(ee + xexpo(s), XF_EZERO);
+}
+
+// alpha[s+1] = (alpha[s] * E + alpha[s][p-1] * Sh[p-1]) (* O); L = pre-shifted shift factors
+template <int K, bool OBS>
+__device__ __forceinline__ void alpha_chain(XRow<K>& A, const XRow<K>& E, const XRow<K>& L,
+                                            const XRow<K>& O) {
+  float hm[K];
+  int he[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    hm[j] = ((j == 0) ? shr_z(A.m[K - 1]) : A.m[j - 1]) * L.m[j];
+    he[j] = ((j == 0) ? shr_z(A.e[K - 1]) : A.e[j - 1]) + L.e[j];
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    chain_add(A.m[j] * E.m[j], A.e[j] + E.e[j], hm[j], he[j], O.m[j], O.e[j], OBS, A.m[j], A.e[j]);
+}
+
+// beta[s] = E * Q[p] + Sh * Q[p+1], Q = beta[s+1] (* O[s+1])
+template <int K, bool OBS>
+__device__ __forceinline__ void beta_chain(XRow<K>& Bt, const XRow<K>& E, const XRow<K>& Sh,
+                                           const XRow<K>& O) {
+  float qm[K];
+  int qe[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    qm[j] = OBS ? Bt.m[j] * O.m[j] : Bt.m[j];
+    qe[j] = OBS ? Bt.e[j] + O.e[j] : Bt.e[j];
+  }
+  float rm[K];
+  int re[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    rm[j] = ((j == K - 1) ? shl_z(qm[0]) : qm[j + 1 < K ? j + 1 : 0]) * Sh.m[j];
+    re[j] = ((j == K - 1) ? shl_z(qe[0]) : qe[j + 1 < K ? j + 1 : 0]) + Sh.e[j];
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    chain_add(E.m[j] * qm[j], E.e[j] + qe[j], rm[j], re[j], 0.0f, 0, false, Bt.m[j], Bt.e[j]);
+}
+
+template <int K>
+__device__ __forceinline__ XRow<K> xrow_zero() {
+  XRow<K> r;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    r.m[j] = 0.0f;
+    r.e[j] = XF_EZERO;
+  }
+  return r;
+}
+
+template <int K>
+__device__ __forceinline__ XRow<K> lds_xrow(const xf* p) {
+  float v[2 * K];
+  ld_vec<2 * K>(v, reinterpret_cast<const float*>(p));
+  return xrow_unpack<K>(v);
+}
+template <int K>
+__device__ __forceinline__ void lds_xrow_st(xf* p, const XRow<K>& r) {
+  float v[2 * K];
+  xrow_pack<K>(r, v);
+  st_vec<2 * K>(reinterpret_cast<float*>(p), v);
+}
+
+template <int K, bool OBS, bool LDS, int kNC, int kNH>
+__global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream(FwdBwdArgs a) {
+  constexpr int kWaves = 2 + 2 * kNC + 2 * kNH;
+  constexpr int R = in_slots<OBS>();
+  constexpr int kR2 = out_slots<OBS>();
+  static_assert(R % kR2 == 0, "ring sizes");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int T = a.T, U = a.U;
+  const int S = a.step_len[b];
+  const int P = a.pos_len[b];
+  const bool term = (a.flags & SSNT_FLAG_TERMINAL_EMIT) != 0;
+  const size_t TU = (size_t)T * U;
+  const float* lt = a.log_trans + (size_t)b * TU * 2;
+  const float* lo = OBS ? a.log_obs + (size_t)b * TU : nullptr;
+  float* g = a.grad ? a.grad + (size_t)b * TU * 2 : nullptr;
+  float* go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
+  float* la = a.log_alpha ? a.log_alpha + (size_t)b * TU : nullptr;
+  float* lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
+  const int p0 = K * lane;
+  const bool act = p0 < U;
+  const int pr = act ? p0 : U - K;  // LDS read position (clamped for lanes past U)
+
+  // ---- LDS: ctl | cut (64K xf) | junk (64 x 16K B) | input rings [2][R] | chain-row rings
+  //      [2][kR2][U xf] | storage rows [T][U xf] (LDS mode)
+  Ctl* ctl = reinterpret_cast<Ctl*>(smem);
+  xf* cutb = reinterpret_cast<xf*>(smem + kCtlBytes);
+  unsigned char* junk = reinterpret_cast<unsigned char*>(cutb + 64 * K);
+  const int slot_bytes = (U * 16 + (OBS ? U * 8 : 0) + 15) & ~15;
+  const int nl16 = (U / K) * 16;  // bytes of one element block of a slot (U % K == 0)
+  unsigned char* inr = junk + 64 * 16 * K;
+  xf* outr = reinterpret_cast<xf*>(inr + 2 * R * slot_bytes);
+  xf* rows = LDS ? outr + 2 * kR2 * U : reinterpret_cast<xf*>(a.workspace) + (size_t)b * TU;
+  unsigned char* junk_lane = junk + 16 * K * lane;
+
+  auto fill_rows = [&](int from, int w0, int wstep) {  // zero grads / -inf debug rows
+    float z[2 * K], ninf[K];
+#pragma unroll
+    for (int j = 0; j < 2 * K; ++j) z[j] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < K; ++j) ninf[j] = -__builtin_inff();
+    for (int s = from + w0; s < T; s += wstep) {
+      if (g) buf_st<2 * K>(z, brsrc(g + (size_t)s * U * 2, U * 8u), p0 * 8);
+      if (go) buf_st<K>(z, brsrc(go + (size_t)s * U, U * 4u), p0 * 4);
+      if (la) buf_st<K>(ninf, brsrc(la + (size_t)s * U, U * 4u), p0 * 4);
+      if (lb) buf_st<K>(ninf, brsrc(lb + (size_t)s * U, U * 4u), p0 * 4);
+    }
+  };
+  const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
+  const bool feasible = S >= 1 && P >= 1 && S <= T && P <= U && S >= P;
+  if (!feasible) {
+    if ((S > T || P > U || S < 0 || P < 0) && a.status && threadIdx.x == 0)
+      atomicOr(a.status, kStatusBadLength);
+    fill_rows(0, wave, kWaves);
+    if (threadIdx.x == 0) a.loss[b] = inf_loss;
+    return;
+  }
+  const int M = (S - 1) >> 1;
+
+  // storage rows: LDS, or this utterance's workspace rows through range-checked buffer ops
+  auto row_st = [&](int s, const XRow<K>& r) {
+    if constexpr (LDS) {
+      lds_xrow_st<K>(act ? rows + (size_t)s * U + p0 : reinterpret_cast<xf*>(junk_lane), r);
+    } else {
+      float v[2 * K];
+      xrow_pack<K>(r, v);
+      buf_st<2 * K>(v, brsrc(rows + (size_t)s * U, U * 8u), p0 * 8);
+    }
+  };
+  auto row_ld = [&](int s) {
+    if constexpr (LDS) {
+      return lds_xrow<K>(rows + (size_t)s * U + pr);
+    } else {
+      float v[2 * K];
+      buf_ld<2 * K>(v, brsrc(rows + (size_t)s * U, U * 8u), pr * 8);
+      return xrow_unpack<K>(v);
+    }
+  };
+  // converted-input slot j of direction d: per position (E.m, E.e, X.m, X.e); obs block after
+
+
+  if (threadIdx.x < kCtlBytes / 4) reinterpret_cast<int*>(smem)[threadIdx.x] = 0;
+  XRow<K> X = xrow_zero<K>();
+  if (wave == 0) {  // alpha[0]: 1 at p = 0 (x obs[0][0])
+    if (lane == 0) {
+      if constexpr (OBS) {
+        const xf o = xf_exp(lo[0], true);
+        const xf n = xf_norm(o.m, o.e);
+        X.m[0] = n.m;
+        X.e[0] = n.e;
+      } else {
+        X.m[0] = 0.5f;
+        X.e[0] = 1;
+      }
+    }
+    row_st(0, X);
+  }
+  __syncthreads();
+  Diag dg;
+
+  if (EXP(7) && (wave < 2 || wave >= 2 + 2 * kNC)) return;  // experiment: converters alone
+  if (wave >= 2 + 2 * kNC) {
+    // =============================== gradient waves ======================================
+    const int d = (wave - 2 - 2 * kNC) & 1;
+    const int h = (wave - 2 - 2 * kNC) >> 1;
+    const int hb = d == 0 ? M : S - M;  // first stream row of this direction's gradient rows
+    const int n_rows = d == 0 ? S - M : M;  // transitions M..S-1 / M-1..0
+    const int nmine = (n_rows - h + kNH - 1) / kNH;
+    // The gradient waves do not touch the converters' rings: they convert their own rows
+    // (log_trans row s, log_obs row s+1 -- L2-hot, the converters streamed them moments ago),
+    // prefetched GD rows ahead, with the same xf_exp arithmetic. Only the chain rows come
+    // from LDS, so the only coupling left is chain progress.
+    constexpr int GD = conv_depth<K>() / 2 > 2 ? conv_depth<K>() / 2 : 2;
+    auto row_of = [&](int i) {
+      const int r = hb + h + kNH * i;
+      return d == 0 ? r : S - 1 - r;
+    };
+    auto gload = [&](int i, Item<K, OBS>& it) {
+      const int s = min(max(row_of(min(i, nmine - 1)), 0), T - 1);
+      buf_ld<2 * K>(it.lt, brsrc(lt + (size_t)s * U * 2, U * 8u), p0 * 8);
+      if constexpr (OBS) {
+        const int orow = min(s + 1, T - 1);
+        buf_ld<K>(it.ob, brsrc(lo + (size_t)orow * U, U * 4u), p0 * 4);
+      }
+    };
+    Item<K, OBS> pf[GD];
+#pragma unroll
+    for (int j = 0; j < GD; ++j) gload(j, pf[j]);
+    // ---- Z at the cut: tree-sum over p of alpha[M][p] * beta[M][p] (fixed order, = oracle)
+    if (d == 0 && h == 0) {
+      spin_until<true>([&] { return ctr_acq(&ctl->a_ready); }, 1, a.status, dg);
+      spin_until<true>([&] { return ctr_acq(&ctl->bm_ready); }, 1, a.status, dg);
+      const XRow<K> Am = row_ld(M);
+      const XRow<K> Bm = lds_xrow<K>(cutb + pr);
+      float wm[K];
+      int we[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        wm[j] = act ? Am.m[j] * Bm.m[j] : 0.0f;
+        we[j] = act ? Am.e[j] + Bm.e[j] : XF_EZERO;
+      }
+#pragma unroll
+      for (int len = K; len > 1; len >>= 1) {
+#pragma unroll
+        for (int i = 0; i < len / 2; ++i) {
+          const xf t = xf_add(wm[2 * i], we[2 * i], wm[2 * i + 1], we[2 * i + 1]);
+          wm[i] = t.m;
+          we[i] = t.e;
+        }
+      }
+      xf z{wm[0], we[0]};
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const float om = __shfl_xor(z.m, off);
+        const int oe = __shfl_xor(z.e, off);
+        z = xf_add(z.m, z.e, om, oe);
+      }
+      if (lane == 0) {
+        ctl->z = z;
+        a.loss[b] = (z.m == 0.0f) ? inf_loss : 0.0f - xf_log(z);
+      }
+      ctr_rel(&ctl->z_ready, 1);
+    } else {
+      spin_until<true>([&] { return ctr_acq(&ctl->z_ready); }, 1, a.status, dg);
+    }
+    dg.mark_cut();
+    const xf Z = ctl->z;
+    const bool zero_z = (Z.m == 0.0f);
+    const float izm = 1.0f / Z.m;
+    const int ize = -Z.e;
+
+    int chain_seen = 0;
+    for (int base = 0; base < nmine; base += GD) {
+#pragma unroll
+      for (int j = 0; j < GD; ++j) {
+        const int i = base + j;
+        [&] {
+          if (i >= nmine) return;
+          const int r = hb + h + kNH * i;  // stream row
+          const int s = row_of(i);         // transition / lattice row
+          const Item<K, OBS>& it = pf[j];
+          // fwd: alpha[s] is written after chain stream row s-1; bwd: beta[s] at stream row r
+          const int need = d == 0 ? r : r + 1;
+          if (chain_seen < need)
+            chain_seen = spin_until<true>([&] { return ctr_ld(&ctl->chain[d]); }, need, a.status, dg);
+          cbar();
+          XRow<K> A, Bn, Bs;
+          if (d == 0) {
+            A = (s == M) ? row_ld(M) : lds_xrow<K>(outr + (size_t)(s % kR2) * U + pr);
+            Bn = row_ld(min(s + 1, S - 1));  // (terminal transition: unused)
+            if (OBS || lb) Bs = (s == M) ? lds_xrow<K>(cutb + pr) : row_ld(s);
+          } else {
+            A = row_ld(s);  // beta[s] is ring row r % kR2 (r = S-1-s), beta[s+1] ring row (r-1)
+            Bn = (s + 1 == M) ? lds_xrow<K>(cutb + pr) : lds_xrow<K>(outr + (size_t)(kR2 + (r - 1) % kR2) * U + pr);
+            if (OBS || lb) Bs = lds_xrow<K>(outr + (size_t)(kR2 + r % kR2) * U + pr);
+          }
+          cbar();
+          ctr_st(&ctl->help[d][h], i + 1);  // ring rows read (in-order DS): reusable
+          if (EXP(0)) return;
+          float ge[2 * K], gob[K];
+          if (zero_z) {
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+              ge[2 * q] = 0.0f;
+              ge[2 * q + 1] = 0.0f;
+              gob[q] = 0.0f;
+            }
+          } else {
+            XRow<K> E, Sh, O;
+            convert<K, OBS>(it, P, lane, E, Sh);
+            convert_obs<K, OBS>(it, P, lane, O);
+            XRow<K> Q, Rr;
+            if (s + 1 < S) {
+#pragma unroll
+              for (int q = 0; q < K; ++q) {
+                Q.m[q] = OBS ? Bn.m[q] * O.m[q] : Bn.m[q];
+                Q.e[q] = OBS ? Bn.e[q] + O.e[q] : Bn.e[q];
+              }
+#pragma unroll
+              for (int q = 0; q < K; ++q) {
+                Rr.m[q] = (q == K - 1) ? shl_z(Q.m[0]) : Q.m[q + 1 < K ? q + 1 : 0];
+                Rr.e[q] = (q == K - 1) ? shl_z(Q.e[0]) : Q.e[q + 1 < K ? q + 1 : 0];
+              }
+            } else {  // terminal transition: only the terminal emit at P-1 (src/lib.rs:187-195)
+#pragma unroll
+              for (int q = 0; q < K; ++q) {
+                const bool lastp = term && (p0 + q) == P - 1;
+                Q.m[q] = lastp ? 1.0f : 0.0f;
+                Q.e[q] = lastp ? 0 : XF_EZERO;
+                Rr.m[q] = 0.0f;
+                Rr.e[q] = XF_EZERO;
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+              const int ae = A.e[q] + ize;  // (integer exponent sums are exact in any order)
+              ge[2 * q] = xf_neg_post(((A.m[q] * E.m[q]) * Q.m[q]) * izm, ae + E.e[q] + Q.e[q]);
+              ge[2 * q + 1] = xf_neg_post(((A.m[q] * Sh.m[q]) * Rr.m[q]) * izm, ae + Sh.e[q] + Rr.e[q]);
+              if constexpr (OBS) gob[q] = xf_neg_post((A.m[q] * Bs.m[q]) * izm, ae + Bs.e[q]);
+            }
+          }
+          if (g) buf_st<2 * K>(ge, brsrc(g + (size_t)s * U * 2, U * 8u), p0 * 8);
+          if constexpr (OBS) {
+            if (go) buf_st<K>(gob, brsrc(go + (size_t)s * U, U * 4u), p0 * 4);
+          }
+          if (la || lb) {  // debug outputs (slow path)
+            float va[K], vb[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+              va[q] = zero_z ? -__builtin_inff() : xf_log(xf{A.m[q], A.e[q]});
+              vb[q] = zero_z ? -__builtin_inff() : xf_log(xf{Bs.m[q], Bs.e[q]});
+            }
+            if (la) buf_st<K>(va, brsrc(la + (size_t)s * U, U * 4u), p0 * 4);
+            if (lb) buf_st<K>(vb, brsrc(lb + (size_t)s * U, U * 4u), p0 * 4);
+          }
+        }();
+        gload(i + GD, pf[j]);  // refill after use, unconditionally (same registers, no copy)
+      }
+    }
+    dg.flush(b, wave);
+    return;
+  }
+
+  if (wave >= 2) {
+    // =============================== converters ==========================================
+    const int d = (wave - 2) & 1;
+    const int c = (wave - 2) >> 1;
+    constexpr int D = conv_depth<K>();
+    const int chain_end = d == 0 ? S - 1 : S;
+    unsigned char* ring = inr + (size_t)d * R * slot_bytes;
+    auto load = [&](int r, Item<K, OBS>& it) {
+      if (EXP(6)) {
+#pragma unroll
+        for (int j = 0; j < 2 * K; ++j) it.lt[j] = -0.5f - 0.01f * r;
+        return;
+      }
+      const int row = min(max(d == 0 ? r : S - 1 - r, 0), T - 1);
+      buf_ld<2 * K>(it.lt, brsrc(lt + (size_t)row * U * 2, U * 8u), p0 * 8);
+      if constexpr (OBS) {
+        const int orow = min(row + 1, T - 1);
+        buf_ld<K>(it.ob, brsrc(lo + (size_t)orow * U, U * 4u), p0 * 4);
+      }
+    };
+    Item<K, OBS> pf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) load(c + kNC * i, pf[i]);
+    int seen_chain = 0;
+    const int nmine = (S - c + kNC - 1) / kNC;  // my stream rows: c, c + kNC, ...
+    for (int base = 0; base < nmine; base += D) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const int k = base + i;
+        if (k < nmine) {
+          const int r = c + kNC * k;
+          const Item<K, OBS>& it = pf[i];
+          XRow<K> E, Sh, O;
+          if (EXP(2)) {  // experiment: no exp() work (timing only)
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              E.m[j] = it.lt[2 * j]; E.e[j] = 0; Sh.m[j] = it.lt[2 * j + 1]; Sh.e[j] = 0;
+              O.m[j] = 1.0f; O.e[j] = 0;
+            }
+          } else {
+            convert<K, OBS>(it, P, lane, E, Sh);
+            convert_obs<K, OBS>(it, P, lane, O);
+          }
+          XRow<K> Xs;
+          if (d == 0) {  // L[p] = Sh[p-1]: canonical zero at p = 0
+            Xs.m[0] = shr1(Sh.m[K - 1]);
+            Xs.e[0] = shr1(Sh.e[K - 1]);
+#pragma unroll
+            for (int j = 1; j < K; ++j) {
+              Xs.m[j] = Sh.m[j - 1];
+              Xs.e[j] = Sh.e[j - 1];
+            }
+          } else {
+            Xs = Sh;
+          }
+          // slot r % R last held row q = r - R: the chain and the gradient waves must be done
+          const int q = r - R;  // (only the chain reads the ring)
+          if (q >= 0 && !EXP(7)) {
+            const int need_c = min(q + 1, chain_end);
+            if (seen_chain < need_c)
+              seen_chain = spin_until<true>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
+          }
+          cbar();
+          unsigned char* sl = ring + (size_t)(r % R) * slot_bytes;
+          float v[4 * K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            v[4 * j] = E.m[j];
+            v[4 * j + 1] = __builtin_bit_cast(float, E.e[j]);
+            v[4 * j + 2] = Xs.m[j];
+            v[4 * j + 3] = __builtin_bit_cast(float, Xs.e[j]);
+          }
+          // planar by element: block q holds (E, X) of positions K*l + q at 16*l -- every
+          // 16-byte lane access is contiguous across the wave (no bank conflicts)
+          if (!EXP(4)) {
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+              st_vec<4>(reinterpret_cast<float*>(act ? sl + (size_t)q * nl16 + 16 * lane : junk_lane + 16 * q), v + 4 * q);
+          }
+          if constexpr (OBS) {
+            float o[2 * K];
+            xrow_pack<K>(O, o);
+            st_vec<2 * K>(reinterpret_cast<float*>(act ? sl + 16 * U + 8 * p0 : junk_lane), o);
+          }
+          cbar();
+          ctr_st(&ctl->conv[d][c], k + 1);
+        }
+        // refill after the old item is consumed: same registers, no copy (a copy of a register
+        // with a load in flight would wait for the load)
+        load(c + kNC * (k + D), pf[i]);
+      }
+    }
+    dg.flush(b, wave);
+    fill_rows(S, d * kNC + c, 2 * kNC);  // zero the rows beyond S
+    return;
+  }
+
+  // ================================== chains =============================================
+  // Unrolled blocks of R steps aligned to R (slot offsets are compile-time); blocks that lie
+  // inside one phase run without per-step guards. Factors for row r+2 are read into row r's
+  // register buffer as soon as row r is done, so a full step hides the LDS latency. All LDS
+  // addresses are per-lane pointers prepared before the loop (lanes past U: junk / clamped).
+  __builtin_amdgcn_s_setprio(3);
+  const int d = wave;
+  int ready = 0;  // stream rows known converted
+  auto wait_row = [&](int r) {  // r: a row that exists
+    if (r >= ready)
+      ready = spin_until<false>([&] { return first_missing<kNC>(ctl->conv[d], 0); }, r + 1, a.status, dg);
+  };
+  const unsigned char* sptr[R];  // slot j, this lane's factors (element block 0)
+#pragma unroll
+  for (int j = 0; j < R; ++j) sptr[j] = inr + (size_t)(d * R + j) * slot_bytes + 16 * (pr / K);
+  xf* optr[kR2];  // chain-row ring row j, this lane (junk past U)
+#pragma unroll
+  for (int j = 0; j < kR2; ++j)
+    optr[j] = act ? outr + (size_t)(d * kR2 + j) * U + p0 : reinterpret_cast<xf*>(junk_lane);
+  auto rd = [&](int j, XRow<K>& E, XRow<K>& Xx, XRow<K>& O) {
+    float v[4 * K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) ld_vec<4>(v + 4 * q, reinterpret_cast<const float*>(sptr[j] + (size_t)q * nl16));
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      E.m[q] = v[4 * q];
+      E.e[q] = __builtin_bit_cast(int, v[4 * q + 1]);
+      Xx.m[q] = v[4 * q + 2];
+      Xx.e[q] = __builtin_bit_cast(int, v[4 * q + 3]);
+    }
+    if constexpr (OBS) {
+      O = lds_xrow<K>(reinterpret_cast<const xf*>(sptr[j] - 16 * (pr / K) + 16 * U) + pr);
+    } else {
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        O.m[q] = 1.0f;
+        O.e[q] = 0;
+      }
+    }
+  };
+  XRow<K> Eb[2], Xb[2], Ob[2];
+  // Steps run in half-blocks of H = R/2 (unrolled by R: slot offsets compile-time). All waits
+  // -- converted rows up to two past the half-block, ring rows released by the gradient waves --
+  // happen at half-block boundaries, so the H steps in between are straight-line code and the
+  // compiler's LDS wait counts stay exact. Progress is published at the end of each half-block
+  // (the rings have the slack: a converter may run R rows ahead of the published progress).
+  constexpr int H = R / 2;
+  auto run = [&](int lo, int hi, auto&& step, auto&& hwait) {
+    for (int base = lo & ~(R - 1); base < hi; base += R) {
+      auto half = [&](auto H0) {
+        constexpr int h0 = decltype(H0)::value;
+        const int hb0 = base + h0;
+        if (hb0 + H <= lo || hb0 >= hi) return;
+        hwait(max(hb0, lo), min(hb0 + H, hi));
+        if (hb0 >= lo && hb0 + H <= hi) {
+          step(std::integral_constant<int, h0 + 0>{}, base, true);
+          step(std::integral_constant<int, h0 + 1>{}, base, true);
+          if constexpr (H > 2) {
+            step(std::integral_constant<int, h0 + 2>{}, base, true);
+            step(std::integral_constant<int, h0 + 3>{}, base, true);
+          }
+        } else {
+          step(std::integral_constant<int, h0 + 0>{}, base, hb0 >= lo && hb0 < hi);
+          step(std::integral_constant<int, h0 + 1>{}, base, hb0 + 1 >= lo && hb0 + 1 < hi);
+          if constexpr (H > 2) {
+            step(std::integral_constant<int, h0 + 2>{}, base, hb0 + 2 >= lo && hb0 + 2 < hi);
+            step(std::integral_constant<int, h0 + 3>{}, base, hb0 + 3 >= lo && hb0 + 3 < hi);
+          }
+        }
+        cbar();
+        ctr_st(&ctl->chain[d], min(hb0 + H, hi));
+        ctr_st(&ctl->sread[d], min(hb0 + H, hi) + 2);  // slot reads run two rows ahead
+      };
+      half(std::integral_constant<int, 0>{});
+      half(std::integral_constant<int, H>{});
+    }
+  };
+  if (d == 0) {
+    // ---------------- alpha chain: stream row r = transition r -> alpha[r+1] --------------
+    const int n = S - 1;
+    const int last = max(n - 1, 0);  // last stream row the chain reads
+    wait_row(min(1, last));
+    cbar();
+    rd(0, Eb[0], Xb[0], Ob[0]);
+    rd(1 % R, Eb[1], Xb[1], Ob[1]);
+    int help_seen = M + 1;  // first alpha ring row not yet released by the gradient waves
+    // storage write pointer for alpha[r+1] (LDS mode)
+    xf* wp = act ? rows + (size_t)U + p0 : reinterpret_cast<xf*>(junk_lane);
+    const int wstep = act ? U : 0;
+    // steps [r0, r1): rows up to r1+1 converted; phase 2: ring rows up to r1-kR2 released
+    auto hwait = [&](int r0, int r1, bool phase2) {
+      (void)r0;
+      wait_row(min(r1 + 1, last));
+      if (phase2) {
+        const int q = r1 - kR2;  // newest previous occupant the half-block overwrites
+        if (q > M && help_seen <= q)
+          help_seen = spin_until<false>([&] { return first_missing<kNH>(ctl->help[0], M); }, q + 1, a.status, dg);
+      }
+      cbar();
+    };
+    auto step = [&](auto Ic, int base, bool live, auto Ph) {
+      constexpr int i = decltype(Ic)::value;
+      constexpr int par = i & 1;
+      constexpr bool phase2 = decltype(Ph)::value;
+      if (!live) return;
+      const int r = base + i;
+      alpha_chain<K, OBS>(X, Eb[par], Xb[par], Ob[par]);
+      if constexpr (!phase2) {
+        if constexpr (LDS) {
+          if (!EXP(5)) lds_xrow_st<K>(wp, X);
+          wp += wstep;
+        } else {
+          row_st(r + 1, X);
+        }
+      } else {
+        lds_xrow_st<K>(optr[(i + 1) % kR2], X);
+      }
+      rd((i + 2) % R, Eb[par], Xb[par], Ob[par]);  // row r+2 (a stale slot past the end is dropped)
+    };
+    if (M == 0) ctr_rel(&ctl->a_ready, 1);
+    ctr_st(&ctl->sread[0], 2);  // slots of rows 0, 1 have been read
+    run(0, M, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::false_type{}); },
+        [&](int r0, int r1) { hwait(r0, r1, false); });
+    if (M > 0) {
+      cbar();
+      ctr_rel(&ctl->a_ready, 1);
+      dg.mark_cut();
+    }
+    run(M, n, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::true_type{}); },
+        [&](int r0, int r1) { hwait(r0, r1, true); });
+  } else {
+    // ---------------- beta chain: stream row r = transition S-1-r -> beta[S-1-r] ----------
+    // beta rows past the cut (s < M) go to ring row r % kR2 (r = S-1-s)
+    const int c = S - 1 - M;  // stream row of the cut (beta[M])
+    const int last = S - 1;
+    wait_row(min(2, last));
+    cbar();
+    rd(0, Eb[0], Xb[0], Ob[0]);
+    rd(1 % R, Eb[1], Xb[1], Ob[1]);
+    int help_seen = S - M;  // first beta gradient row (stream rows) not finished
+    xf* wp = act ? rows + (size_t)(S - 1) * U + p0 : reinterpret_cast<xf*>(junk_lane);  // beta[S-1-r]
+    const int wstep = act ? U : 0;
+    // stream row r -> kind 0: storage row S-1-r; 1: cut buffer; 2: ring row r % kR2
+    auto put = [&](int r, int i, auto Kd) {
+      constexpr int kind = decltype(Kd)::value;
+      if constexpr (kind == 0) {
+        if constexpr (LDS) {
+          if (!EXP(5)) lds_xrow_st<K>(wp, X);
+        } else {
+          row_st(S - 1 - r, X);
+        }
+      } else if constexpr (kind == 1) {
+        lds_xrow_st<K>(act ? cutb + p0 : reinterpret_cast<xf*>(junk_lane), X);
+        cbar();
+        ctr_rel(&ctl->bm_ready, 1);
+        dg.mark_cut();
+      } else {
+        lds_xrow_st<K>(optr[i % kR2], X);
+      }
+      wp -= wstep;
+    };
+    auto hwait = [&](int r0, int r1, bool ring) {
+      (void)r0;
+      wait_row(min(r1 + 1, last));
+      if (ring) {
+        // previous occupants: stream rows up to r1-1-kR2, read by gradient rows q and q+1
+        const int q = r1 - 1 - kR2;
+        if (q > c && help_seen <= q + 1)
+          help_seen = spin_until<false>([&] { return first_missing<kNH>(ctl->help[1], S - M); }, q + 2, a.status, dg);
+      }
+      cbar();
+    };
+#pragma unroll
+    for (int j = 0; j < K; ++j) {  // beta[S-1]: terminal emit (src/lib.rs:187-195)
+      const bool lastp = (p0 + j) == P - 1;
+      const xf v = term ? xf_norm(Eb[0].m[j], Eb[0].e[j]) : xf{0.5f, 1};
+      X.m[j] = lastp ? v.m : 0.0f;
+      X.e[j] = lastp ? v.e : XF_EZERO;
+    }
+    if (c == 0) put(0, 0, std::integral_constant<int, 1>{});
+    else put(0, 0, std::integral_constant<int, 0>{});
+    cbar();
+    rd(2 % R, Eb[0], Xb[0], Ob[0]);
+    auto step = [&](auto Ic, int base, bool live, auto Kd) {
+      constexpr int i = decltype(Ic)::value;
+      constexpr int par = i & 1;
+      if (!live) return;
+      const int r = base + i;
+      beta_chain<K, OBS>(X, Eb[par], Xb[par], Ob[par]);
+      put(r, i, Kd);
+      rd((i + 2) % R, Eb[par], Xb[par], Ob[par]);
+    };
+    cbar();
+    ctr_st(&ctl->chain[1], 1);  // stream row 0 (the terminal row) is done
+    ctr_st(&ctl->sread[1], 3);  // slots of rows 0..2 have been read
+    run(1, c, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 0>{}); },
+        [&](int r0, int r1) { hwait(r0, r1, false); });
+    if (c >= 1)
+      run(c, c + 1, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 1>{}); },
+          [&](int r0, int r1) { hwait(r0, r1, false); });
+    run(c + 1, S, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 2>{}); },
+        [&](int r0, int r1) { hwait(r0, r1, true); });
+  }
+  dg.flush(b, wave);
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <int K, bool OBS, bool LDS, int NC, int NH>
+int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
+  auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH>;
+  if (lds > 64 * 1024) {  // dynamic LDS above 64 KiB needs the attribute (idempotent)
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(64 * (2 + 2 * NC + 2 * NH)), lds, st, a);
+  return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
+}
+
+template <int K, bool OBS, int NC, int NH>
+int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
+  // whole lane slices and 16-byte aligned tensors (the kernel's vector accesses)
+  const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
+                   aligned16(a.grad) && aligned16(a.grad_obs) && aligned16(a.log_alpha) &&
+                   aligned16(a.log_beta) && aligned16(a.workspace);
+  if (!vec) return SSNT_ERR_UNSUPPORTED;
+  const size_t head = stream_head_bytes(K, a.U, OBS);
+  if (head > kLdsBudget) return SSNT_ERR_UNSUPPORTED;
+  const size_t rows = (size_t)a.T * a.U * sizeof(xf);
+  const bool lds = head + rows <= kLdsBudget;
+  if (!lds && (a.workspace == nullptr || a.workspace_bytes < (size_t)a.B * rows))
+    return SSNT_ERR_WORKSPACE;
+  return lds ? launch_stream_kernel<K, OBS, true, NC, NH>(a, head + rows, st)
+             : launch_stream_kernel<K, OBS, false, NC, NH>(a, head, st);
+}
+
+template <bool OBS, int NC, int NH>
+int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
+#ifdef SSNT_EXP
+  if (OBS || a.U <= 64 || a.U > 128) return SSNT_ERR_UNSUPPORTED;
+  return launch_stream_k<2, false, NC, NH>(a, st);
+#else
+  if (a.U <= 64) return launch_stream_k<1, OBS, NC, NH>(a, st);
+  if (a.U <= 128) return launch_stream_k<2, OBS, NC, NH>(a, st);
+  if (a.U <= 256) return launch_stream_k<4, OBS, NC, NH>(a, st);
+  if (a.U <= 512) return launch_stream_k<8, OBS, NC, NH>(a, st);
+  return SSNT_ERR_UNSUPPORTED;
+#endif
+}
+
+}  // namespace
+
+int diag_read(void* host, size_t bytes) {
+#ifdef SSNT_DIAG
+  if (bytes > sizeof(g_diag)) bytes = sizeof(g_diag);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? (int)bytes : -1;
+#else
+  (void)host;
+  (void)bytes;
+  return -1;
+#endif
+}
+
+size_t stream_head_bytes(int K, int U, bool obs) {
+  const int R = obs ? in_slots<true>() : in_slots<false>();
+  const int R2 = obs ? out_slots<true>() : out_slots<false>();
+  const size_t slot = ((size_t)U * 16 + (obs ? (size_t)U * 8 : 0) + 15) & ~(size_t)15;
+  return kCtlBytes + (size_t)64 * K * sizeof(xf) + (size_t)64 * 16 * K + 2 * (size_t)R * slot +
+         2 * (size_t)R2 * U * sizeof(xf);
+}
+
+int g_mix = 0;  // tuning knob (ssnt_fwd_bwd_set_variant >= 2)
+
+int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
+  if (g_mix == 1) return a.log_obs ? launch_stream_obs<true, 2, 2>(a, st) : launch_stream_obs<false, 2, 2>(a, st);
+  if (g_mix == 2) return a.log_obs ? launch_stream_obs<true, 3, 2>(a, st) : launch_stream_obs<false, 3, 2>(a, st);
+  return a.log_obs ? launch_stream_obs<true, 4, 2>(a, st) : launch_stream_obs<false, 4, 2>(a, st);
+}
+
+void set_stream_mix(int m) { g_mix = m; }
+
+}  // namespace ssnt

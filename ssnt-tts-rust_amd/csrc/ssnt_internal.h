@@ -14,6 +14,7 @@ constexpr int kStatusNoCandidate = 1 << 0;       // v2: no duration sequence fit
 constexpr int kStatusDurationMismatch = 1 << 1;  // upsample: sum(d) != output_length (src/v2_util.rs:58)
 constexpr int kStatusBadLength = 1 << 2;         // fwd-bwd: step/pos length outside the tensor
 constexpr int kStatusBadIndex = 1 << 3;          // backtrace: branch index outside [0, W)
+constexpr int kStatusTimeout = 1 << 4;           // fwd-bwd: an intra-workgroup wait hit its bound
 
 int status_bits_to_code(int bits);
 
@@ -32,11 +33,16 @@ struct FwdBwdArgs {
   void* workspace;   // row storage when the rows do not fit LDS
   size_t workspace_bytes;
   int* status;  // device status word or null
+  int exp;      // experiment knobs (SSNT_EXP builds only; 0 in the product)
 };
 size_t fwd_bwd_workspace_bytes(int B, int T, int U);
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
 int set_fwd_bwd_variant(int v);
-int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only
+// streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take
+int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t stream);
+void set_stream_mix(int m);  // tuning only
+size_t stream_head_bytes(int K, int U, bool obs);  // LDS bytes besides the lattice rows
+int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only (tools/diag_fwd_bwd.py)
 
 // ---- beam-search decode (decode.hip) ----
 enum class Variant : int { V1 = 0, V2 = 1, Tone = 2 };

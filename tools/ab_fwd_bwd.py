@@ -14,7 +14,7 @@ sys.path.insert(0, str(ROOT / "ssnt-tts-rust_amd"))
 import ssnt_tts_amd as S  # noqa: E402
 
 
-def bench_shape(B, T, U, variants=(0, 2, 3, 1), rounds=5, iters=10):
+def bench_shape(B, T, U, variants=(0, 1, 2, 3), rounds=5, iters=10):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(0)
@@ -37,7 +37,8 @@ def bench_shape(B, T, U, variants=(0, 2, 3, 1), rounds=5, iters=10):
         for v in variants:
             lib.ssnt_fwd_bwd_set_variant(v)
             for _ in range(2):
-                assert lib.ssnt_fwd_bwd_device(*args) == 0
+                rc = lib.ssnt_fwd_bwd_device(*args)
+                assert rc == 0, f"variant {v}: status {rc}"
             torch.cuda.synchronize()
             if rnd == 0:
                 out = (loss.clone(), grad.clone())
