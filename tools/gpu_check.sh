@@ -6,7 +6,7 @@ TAG=${1:-r1}
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 420 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu_${TAG}.log 2>&1
+timeout -k 10 420 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_${TAG}.log 2>&1
 tail -3 gpurun_out/pytest_gpu_${TAG}.log
 timeout -k 10 300 python3 bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
 cat gpurun_out/bench_${TAG}.json
