@@ -35,6 +35,7 @@
 #include <limits.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "lattice_dev.h"
 
@@ -91,20 +92,24 @@ __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 // Diagnostic build only (-DSSNT_DIAG, `make lib-diag`): per-wave s_memtime totals, read back
 // with ssnt_diag_read() (tools/diag_fwd_bwd.py). g_diag[b][wave][8]: 0 total cycles, 1 cycles
 // spent spinning, 2 spins that waited, 3 cycle of the cut (chains: alpha[M] / beta[M] stored;
-// gradient waves: Z known). Never present in the product build.
+// gradient waves: Z known), 4 cycles spent spinning before the cut. Never present in the product build.
 #ifdef SSNT_DIAG
 __device__ unsigned long long g_diag[1024][2 + 4 * kMaxW][8];
 struct Diag {
-  unsigned long long t0 = __builtin_amdgcn_s_memtime(), wait = 0, cut = 0;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime(), wait = 0, cut = 0, cut_wait = 0;
   unsigned long long n = 0;
   __device__ unsigned long long now() const { return __builtin_amdgcn_s_memtime(); }
-  __device__ void mark_cut() { cut = now() - t0; }
+  __device__ void mark_cut() {
+    cut = now() - t0;
+    cut_wait = wait;
+  }
   __device__ void flush(int b, int w) {
     if ((threadIdx.x & 63) == 0 && b < 1024) {
       g_diag[b][w][0] = now() - t0;
       g_diag[b][w][1] = wait;
       g_diag[b][w][2] = n;
       g_diag[b][w][3] = cut;
+      g_diag[b][w][4] = cut_wait;
     }
   }
 };
@@ -143,6 +148,16 @@ __device__ __forceinline__ int first_missing(const int* cnt, int begin) {
 #pragma unroll
   for (int w = 0; w < NW; ++w) m = min(m, begin + w + NW * ctr_ld(cnt + w));
   return m;
+}
+
+// compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>)
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // neighbour moves with zero fill at the wave edge (bound_ctrl): foldable into the consumer
@@ -344,26 +359,16 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     const int hb = d == 0 ? M : S - M;  // first stream row of this direction's gradient rows
     const int n_rows = d == 0 ? S - M : M;  // transitions M..S-1 / M-1..0
     const int nmine = (n_rows - h + kNH - 1) / kNH;
-    // The gradient waves do not touch the converters' rings: they convert their own rows
-    // (log_trans row s, log_obs row s+1 -- L2-hot, the converters streamed them moments ago),
-    // prefetched GD rows ahead, with the same xf_exp arithmetic. Only the chain rows come
-    // from LDS, so the only coupling left is chain progress.
-    constexpr int GD = conv_depth<K>() / 2 > 2 ? conv_depth<K>() / 2 : 2;
+    // The gradient waves take their (E, Sh) factors from the converters' input ring: the slot
+    // of stream row r holds exactly the factors of that row (the forward ring holds the
+    // pre-shifted L[p] = Sh[p-1], undone here with one DPP). Each cell is therefore converted
+    // once per direction, and these waves issue no global loads at all: their only vector
+    // memory instructions are the gradient stores. The converters keep a slot until the
+    // gradient waves of its row have read it (help counters).
     auto row_of = [&](int i) {
       const int r = hb + h + kNH * i;
       return d == 0 ? r : S - 1 - r;
     };
-    auto gload = [&](int i, Item<K, OBS>& it) {
-      const int s = min(max(row_of(min(i, nmine - 1)), 0), T - 1);
-      buf_ld<2 * K>(it.lt, brsrc(lt + (size_t)s * U * 2, U * 8u), p0 * 8);
-      if constexpr (OBS) {
-        const int orow = min(s + 1, T - 1);
-        buf_ld<K>(it.ob, brsrc(lo + (size_t)orow * U, U * 4u), p0 * 4);
-      }
-    };
-    Item<K, OBS> pf[GD];
-#pragma unroll
-    for (int j = 0; j < GD; ++j) gload(j, pf[j]);
     // ---- Z at the cut: tree-sum over p of alpha[M][p] * beta[M][p] (fixed order, = oracle)
     if (d == 0 && h == 0) {
       spin_until<true>([&] { return ctr_acq(&ctl->a_ready); }, 1, a.status, dg);
@@ -407,34 +412,59 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     const float izm = 1.0f / Z.m;
     const int ize = -Z.e;
 
+    // Rows are software-pipelined: row i+1's LDS reads are issued before row i's arithmetic
+    // whenever the chain is already known to be past row i+1 (the steady state -- these waves
+    // trail the chain), so a row costs its arithmetic, not an LDS round trip.
+    struct GIn {
+      XRow<K> A, Bn, Bs, E, Sh, O;
+    };
     int chain_seen = 0;
-    for (int base = 0; base < nmine; base += GD) {
+    auto need_of = [&](int i) {  // fwd: alpha[s] is written after chain stream row s-1;
+      const int r = hb + h + kNH * i;  // bwd: beta[s] at stream row r
+      return d == 0 ? r : r + 1;
+    };
+    auto wait_chain = [&](int i) {
+      const int need = need_of(i);
+      if (chain_seen < need)
+        chain_seen = spin_until<true>([&] { return ctr_ld(&ctl->chain[d]); }, need, a.status, dg);
+      cbar();
+    };
+    auto fetch = [&](int i, GIn& in) {
+      const int r = hb + h + kNH * i;  // stream row
+      const int s = row_of(i);         // transition / lattice row
+      const unsigned char* sl = inr + (size_t)(d * R + r % R) * slot_bytes;  // factors of row r
+      float v[4 * K];
 #pragma unroll
-      for (int j = 0; j < GD; ++j) {
-        const int i = base + j;
-        [&] {
-          if (i >= nmine) return;
-          const int r = hb + h + kNH * i;  // stream row
-          const int s = row_of(i);         // transition / lattice row
-          const Item<K, OBS>& it = pf[j];
-          // fwd: alpha[s] is written after chain stream row s-1; bwd: beta[s] at stream row r
-          const int need = d == 0 ? r : r + 1;
-          if (chain_seen < need)
-            chain_seen = spin_until<true>([&] { return ctr_ld(&ctl->chain[d]); }, need, a.status, dg);
-          cbar();
-          XRow<K> A, Bn, Bs;
-          if (d == 0) {
-            A = (s == M) ? row_ld(M) : lds_xrow<K>(outr + (size_t)(s % kR2) * U + pr);
-            Bn = row_ld(min(s + 1, S - 1));  // (terminal transition: unused)
-            if (OBS || lb) Bs = (s == M) ? lds_xrow<K>(cutb + pr) : row_ld(s);
-          } else {
-            A = row_ld(s);  // beta[s] is ring row r % kR2 (r = S-1-s), beta[s+1] ring row (r-1)
-            Bn = (s + 1 == M) ? lds_xrow<K>(cutb + pr) : lds_xrow<K>(outr + (size_t)(kR2 + (r - 1) % kR2) * U + pr);
-            if (OBS || lb) Bs = lds_xrow<K>(outr + (size_t)(kR2 + r % kR2) * U + pr);
-          }
-          cbar();
-          ctr_st(&ctl->help[d][h], i + 1);  // ring rows read (in-order DS): reusable
-          if (EXP(0)) return;
+      for (int q = 0; q < K; ++q)
+        ld_vec<4>(v + 4 * q, reinterpret_cast<const float*>(sl + (size_t)q * nl16 + 16 * (pr / K)));
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        in.E.m[q] = v[4 * q];
+        in.E.e[q] = __builtin_bit_cast(int, v[4 * q + 1]);
+        in.Sh.m[q] = v[4 * q + 2];
+        in.Sh.e[q] = __builtin_bit_cast(int, v[4 * q + 3]);
+      }
+      if constexpr (OBS) in.O = lds_xrow<K>(reinterpret_cast<const xf*>(sl + 16 * U) + pr);
+      if (d == 0) {
+        in.A = (s == M) ? row_ld(M) : lds_xrow<K>(outr + (size_t)(s % kR2) * U + pr);
+        in.Bn = row_ld(min(s + 1, S - 1));  // (terminal transition: unused)
+        if (OBS || lb) in.Bs = (s == M) ? lds_xrow<K>(cutb + pr) : row_ld(s);
+      } else {
+        in.A = row_ld(s);  // beta[s] is ring row r % kR2 (r = S-1-s), beta[s+1] ring row (r-1)
+        in.Bn = (s + 1 == M) ? lds_xrow<K>(cutb + pr) : lds_xrow<K>(outr + (size_t)(kR2 + (r - 1) % kR2) * U + pr);
+        if (OBS || lb) in.Bs = lds_xrow<K>(outr + (size_t)(kR2 + r % kR2) * U + pr);
+      }
+      cbar();
+      ctr_st(&ctl->help[d][h], i + 1);  // ring rows read (in-order DS): reusable
+    };
+    auto emit = [&](int i, const GIn& in) {
+          const int s = row_of(i);
+          const XRow<K>& A = in.A;
+          const XRow<K>& Bn = in.Bn;
+          const XRow<K>& Bs = in.Bs;
+          const XRow<K>& E = in.E;
+          const XRow<K>& O = in.O;
+          XRow<K> Sh = in.Sh;
           float ge[2 * K], gob[K];
           if (zero_z) {
 #pragma unroll
@@ -444,9 +474,17 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
               gob[q] = 0.0f;
             }
           } else {
-            XRow<K> E, Sh, O;
-            convert<K, OBS>(it, P, lane, E, Sh);
-            convert_obs<K, OBS>(it, P, lane, O);
+            if (d == 0) {  // Sh[p] = L[p+1]; masked (exact zero) for p >= P-1 (src/lib.rs:196-205)
+              XRow<K> L = Sh;
+#pragma unroll
+              for (int q = 0; q < K; ++q) {
+                const float lm = (q == K - 1) ? shl_z(L.m[0]) : L.m[q + 1 < K ? q + 1 : 0];
+                const int le = (q == K - 1) ? shl_z(L.e[0]) : L.e[q + 1 < K ? q + 1 : 0];
+                const bool live = p0 + q < P - 1;
+                Sh.m[q] = live ? lm : 0.0f;
+                Sh.e[q] = live ? le : XF_EZERO;
+              }
+            }
             XRow<K> Q, Rr;
             if (s + 1 < S) {
 #pragma unroll
@@ -477,7 +515,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
               if constexpr (OBS) gob[q] = xf_neg_post((A.m[q] * Bs.m[q]) * izm, ae + Bs.e[q]);
             }
           }
-          if (g) buf_st<2 * K>(ge, brsrc(g + (size_t)s * U * 2, U * 8u), p0 * 8);
+          if (g && !EXP(1)) buf_st<2 * K>(ge, brsrc(g + (size_t)s * U * 2, U * 8u), p0 * 8);
           if constexpr (OBS) {
             if (go) buf_st<K>(gob, brsrc(go + (size_t)s * U, U * 4u), p0 * 4);
           }
@@ -491,9 +529,25 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
             if (la) buf_st<K>(va, brsrc(la + (size_t)s * U, U * 4u), p0 * 4);
             if (lb) buf_st<K>(vb, brsrc(lb + (size_t)s * U, U * 4u), p0 * 4);
           }
-        }();
-        gload(i + GD, pf[j]);  // refill after use, unconditionally (same registers, no copy)
+    };
+    auto row = [&](int i, GIn& cur, GIn& nxt) {
+      const bool more = i + 1 < nmine;
+      const bool early = more && chain_seen >= need_of(i + 1);
+      if (early) fetch(i + 1, nxt);
+      if (!EXP(0)) emit(i, cur);  // experiment: rows fetched and released, no gradient work
+      if (more && !early) {
+        wait_chain(i + 1);
+        fetch(i + 1, nxt);
       }
+    };
+    GIn gin0, gin1;  // alternating buffers (no register copies of rows with reads in flight)
+    if (nmine > 0) {
+      wait_chain(0);
+      fetch(0, gin0);
+    }
+    for (int i = 0; i < nmine; i += 2) {
+      row(i, gin0, gin1);
+      if (i + 1 < nmine) row(i + 1, gin1, gin0);
     }
     dg.flush(b, wave);
     return;
@@ -523,6 +577,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 #pragma unroll
     for (int i = 0; i < D; ++i) load(c + kNC * i, pf[i]);
     int seen_chain = 0;
+    const int hb = d == 0 ? M : S - M;  // first stream row the gradient waves read
+    int seen_grad = hb;
     const int nmine = (S - c + kNC - 1) / kNC;  // my stream rows: c, c + kNC, ...
     for (int base = 0; base < nmine; base += D) {
 #pragma unroll
@@ -555,11 +611,13 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
             Xs = Sh;
           }
           // slot r % R last held row q = r - R: the chain and the gradient waves must be done
-          const int q = r - R;  // (only the chain reads the ring)
+          const int q = r - R;  // (read by the chain, and by the gradient waves from row hb on)
           if (q >= 0 && !EXP(7)) {
             const int need_c = min(q + 1, chain_end);
             if (seen_chain < need_c)
               seen_chain = spin_until<true>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
+            if (q >= hb && seen_grad <= q)
+              seen_grad = spin_until<true>([&] { return first_missing<kNH>(ctl->help[d], hb); }, q + 1, a.status, dg);
           }
           cbar();
           unsigned char* sl = ring + (size_t)(r % R) * slot_bytes;
@@ -642,35 +700,32 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // happen at half-block boundaries, so the H steps in between are straight-line code and the
   // compiler's LDS wait counts stay exact. Progress is published at the end of each half-block
   // (the rings have the slack: a converter may run R rows ahead of the published progress).
-  constexpr int H = R / 2;
-  auto run = [&](int lo, int hi, auto&& step, auto&& hwait) {
+  // Phase 2 (past the cut) publishes every H2 steps instead: there the gradient waves read each
+  // factor slot right behind the chain and the converters need it back, so the hand-off
+  // chain -> gradient waves -> converters -> chain has to close within the ring's slack.
+  using H1 = std::integral_constant<int, R / 2>;
+  using H2 = std::integral_constant<int, (R / 4 > 2 ? R / 4 : 2)>;
+  auto run = [&](auto Hc, int lo, int hi, auto&& step, auto&& hwait) {
+    constexpr int HS = decltype(Hc)::value;
+    static_assert(R % HS == 0, "sub-blocks tile the ring");
     for (int base = lo & ~(R - 1); base < hi; base += R) {
-      auto half = [&](auto H0) {
-        constexpr int h0 = decltype(H0)::value;
+      sfor<R / HS>([&](auto Q) {
+        constexpr int h0 = decltype(Q)::value * HS;
         const int hb0 = base + h0;
-        if (hb0 + H <= lo || hb0 >= hi) return;
-        hwait(max(hb0, lo), min(hb0 + H, hi));
-        if (hb0 >= lo && hb0 + H <= hi) {
-          step(std::integral_constant<int, h0 + 0>{}, base, true);
-          step(std::integral_constant<int, h0 + 1>{}, base, true);
-          if constexpr (H > 2) {
-            step(std::integral_constant<int, h0 + 2>{}, base, true);
-            step(std::integral_constant<int, h0 + 3>{}, base, true);
-          }
+        if (hb0 + HS <= lo || hb0 >= hi) return;
+        hwait(max(hb0, lo), min(hb0 + HS, hi));
+        if (hb0 >= lo && hb0 + HS <= hi) {
+          sfor<HS>([&](auto J) { step(std::integral_constant<int, h0 + decltype(J)::value>{}, base, true); });
         } else {
-          step(std::integral_constant<int, h0 + 0>{}, base, hb0 >= lo && hb0 < hi);
-          step(std::integral_constant<int, h0 + 1>{}, base, hb0 + 1 >= lo && hb0 + 1 < hi);
-          if constexpr (H > 2) {
-            step(std::integral_constant<int, h0 + 2>{}, base, hb0 + 2 >= lo && hb0 + 2 < hi);
-            step(std::integral_constant<int, h0 + 3>{}, base, hb0 + 3 >= lo && hb0 + 3 < hi);
-          }
+          sfor<HS>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            step(std::integral_constant<int, h0 + j>{}, base, hb0 + j >= lo && hb0 + j < hi);
+          });
         }
         cbar();
-        ctr_st(&ctl->chain[d], min(hb0 + H, hi));
-        ctr_st(&ctl->sread[d], min(hb0 + H, hi) + 2);  // slot reads run two rows ahead
-      };
-      half(std::integral_constant<int, 0>{});
-      half(std::integral_constant<int, H>{});
+        ctr_st(&ctl->chain[d], min(hb0 + HS, hi));
+        ctr_st(&ctl->sread[d], min(hb0 + HS, hi) + 2);  // slot reads run two rows ahead
+      });
     }
   };
   if (d == 0) {
@@ -717,14 +772,14 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     };
     if (M == 0) ctr_rel(&ctl->a_ready, 1);
     ctr_st(&ctl->sread[0], 2);  // slots of rows 0, 1 have been read
-    run(0, M, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::false_type{}); },
+    run(H1{}, 0, M, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::false_type{}); },
         [&](int r0, int r1) { hwait(r0, r1, false); });
     if (M > 0) {
       cbar();
       ctr_rel(&ctl->a_ready, 1);
       dg.mark_cut();
     }
-    run(M, n, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::true_type{}); },
+    run(H2{}, M, n, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::true_type{}); },
         [&](int r0, int r1) { hwait(r0, r1, true); });
   } else {
     // ---------------- beta chain: stream row r = transition S-1-r -> beta[S-1-r] ----------
@@ -791,12 +846,12 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     cbar();
     ctr_st(&ctl->chain[1], 1);  // stream row 0 (the terminal row) is done
     ctr_st(&ctl->sread[1], 3);  // slots of rows 0..2 have been read
-    run(1, c, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 0>{}); },
+    run(H1{}, 1, c, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 0>{}); },
         [&](int r0, int r1) { hwait(r0, r1, false); });
     if (c >= 1)
-      run(c, c + 1, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 1>{}); },
+      run(H1{}, c, c + 1, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 1>{}); },
           [&](int r0, int r1) { hwait(r0, r1, false); });
-    run(c + 1, S, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 2>{}); },
+    run(H2{}, c + 1, S, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 2>{}); },
         [&](int r0, int r1) { hwait(r0, r1, true); });
   }
   dg.flush(b, wave);
@@ -875,9 +930,18 @@ size_t stream_head_bytes(int K, int U, bool obs) {
 int g_mix = 0;  // tuning knob (ssnt_fwd_bwd_set_variant >= 2)
 
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
-  if (g_mix == 1) return a.log_obs ? launch_stream_obs<true, 2, 2>(a, st) : launch_stream_obs<false, 2, 2>(a, st);
-  if (g_mix == 2) return a.log_obs ? launch_stream_obs<true, 3, 2>(a, st) : launch_stream_obs<false, 3, 2>(a, st);
-  return a.log_obs ? launch_stream_obs<true, 4, 2>(a, st) : launch_stream_obs<false, 4, 2>(a, st);
+  // tuning mixes (ssnt_fwd_bwd_set_variant >= 2): K = 2 without log_obs only, else the default
+  if (g_mix != 0 && !a.log_obs && a.U > 64 && a.U <= 128) {
+    switch (g_mix) {
+      case 1: return launch_stream_k<2, false, 4, 2>(a, st);
+      case 2: return launch_stream_k<2, false, 3, 2>(a, st);
+      case 3: return launch_stream_k<2, false, 2, 4>(a, st);
+      case 4: return launch_stream_k<2, false, 2, 2>(a, st);
+      case 5: return launch_stream_k<2, false, 2, 3>(a, st);
+      default: break;
+    }
+  }
+  return a.log_obs ? launch_stream_obs<true, 3, 3>(a, st) : launch_stream_obs<false, 3, 3>(a, st);
 }
 
 void set_stream_mix(int m) { g_mix = m; }

@@ -150,3 +150,22 @@ def test_autograd_function(gpu, oracle):
     assert np.array_equal(loss.detach().cpu().numpy(), o["loss"])
     want = o["grad"] * np.array([1.0, 2.0, 0.5], np.float32)[:, None, None, None]
     assert np.array_equal(x.grad.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6])
+def test_tuning_wave_mixes_bit_exact(gpu, oracle, kernel_variant, variant):
+    # the converter / gradient wave mixes of the streaming kernel (ssnt_fwd_bwd_set_variant 2..6,
+    # K = 2 shapes) must be bit-identical to the oracle like the default mix
+    if kernel_variant != 0:
+        pytest.skip("mix variants are streaming-kernel variants")
+    lib = gpu.load()
+    assert lib.ssnt_fwd_bwd_set_variant(variant) == 0
+    rng = np.random.default_rng(variant)
+    B, T, U = 6, 90, 80
+    P = rng.integers(1, U + 1, size=B)
+    S = np.array([rng.integers(max(1, p), T + 1) for p in P])
+    S[0], P[0] = T, U
+    lt = oracle.synth_log_trans(B, T, U, seed=100 + variant)
+    g = _run_gpu(gpu, lt, S, P)
+    o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
+    _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])

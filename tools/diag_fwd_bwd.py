@@ -14,11 +14,13 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import ssnt_tts_amd as S  # noqa: E402
 
-NC, NH = (int(x) for x in os.environ.get("SSNT_DIAG_MIX", "4,2").split(","))
+VARIANT = int(os.environ.get("SSNT_VARIANT", "0"))  # 0 default mix, 2..6 tuning mixes
+NC, NH = {0: (3, 3), 2: (4, 2), 3: (3, 2), 4: (2, 4), 5: (2, 2), 6: (2, 3)}[VARIANT]
 ROLES = ["alpha chain", "beta chain"] + [f"conv {'fb'[i % 2]}{i // 2}" for i in range(2 * NC)] + \
         [f"grad {'fb'[i % 2]}{i // 2}" for i in range(2 * NH)]
 B, T, U = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (256, 200, 80)))
 lib = S.load()
+assert lib.ssnt_fwd_bwd_set_variant(VARIANT) == 0
 lib.ssnt_diag_read.restype = ctypes.c_int
 lib.ssnt_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 dev = torch.device("cuda:0")
@@ -43,6 +45,6 @@ for _ in range(5):
     times.append(e0.elapsed_time(e1) * 1e3)
 print(f"exp={os.environ.get('SSNT_EXP', '0')} launch (incl. wrapper) median {np.median(times):.1f} us")
 for w, nm in enumerate(ROLES):
-    tot, wait, nw, cut = (np.median(d[:, w, i]) for i in range(4))
+    tot, wait, nw, cut, cw = (np.median(d[:, w, i]) for i in range(5))
     print(f"{nm:12s} total {tot:8.0f}  spinning {wait:8.0f} ({nw:4.0f} spins)  cut@ {cut:8.0f}"
-          f"  per-step {tot / T:6.1f}")
+          f" (spun {cw:7.0f} before)  per-step {tot / T:6.1f}")
