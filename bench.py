@@ -4,13 +4,15 @@
 Workload (BASELINE.json configs[1], and configs[3] at N=8): per GPU B=256 utterances,
 T=200 steps x U=80 positions, f32 log_trans (B,T,U,2) = log_softmax over {emit, shift} of
 z ~ N(0, 1.5^2) (synthetic, generated on device, seed = rank). One step = one fused
-fwd-bwd launch through the C-ABI (ssnt_fwd_bwd_device) writing loss (B) and grad (B,T,U,2),
-plus the per-shard loss sum and, for N > 1, an RCCL all-reduce of that scalar over xGMI.
+fwd-bwd launch through the C-ABI (ssnt_fwd_bwd_sum_device) writing loss (B), grad (B,T,U,2)
+and the shard's loss sum (formed in the same launch), plus, for N > 1, an RCCL all-reduce of
+that scalar over xGMI.
 Weak scaling: per-GPU work is fixed. value = all ranks' lattice cells / max-over-ranks time.
 
 roofline: algorithmic HBM bytes of the fwd-bwd kernel = 16 B/cell (read 2xf32 log_trans, write
 2xf32 grad) x cells per launch, over the kernel's average duration measured
-with HIP events on the launch stream inside the timed region; peak 8 TB/s (MI355X_MICROARCH.md).
+with HIP events on the launch stream around the K back-to-back launches of the timed region
+(so it includes the ~1 us gaps between launches); peak 8 TB/s (MI355X_MICROARCH.md).
 traffic: HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
 null when absent.
 cpu_baseline: the C oracle (oracle/ssnt_oracle.c, same split-exponent arithmetic; the reference
@@ -91,73 +93,113 @@ def main():
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--U", type=int, default=80)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse "
+                    "the multi-rank path on a one-GPU box")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    local = local % max(1, torch.cuda.device_count())  # (rehearsal: several ranks on one GPU)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if dist:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(args.dist_backend)
 
     B, T, U = args.batch, args.T, args.U
     lt = synth(B, T, U, seed=rank, dev=dev)
     sl = torch.full((B,), T, dtype=torch.int32, device=dev)
     pl = torch.full((B,), U, dtype=torch.int32, device=dev)
     out = {"loss": torch.empty(B, device=dev), "grad": torch.empty((B, T, U, 2), device=dev),
-           "status": torch.zeros(1, dtype=torch.int32, device=dev)}
-    total = torch.zeros(1, device=dev)
-    # correctness/status check once through the full Python mirror, outside the timed region
-    r = S.ssnt_fwd_bwd(lt, sl, pl, out=out, check=True)
-    assert torch.isfinite(r["loss"]).all()
+           "status": torch.zeros(1, dtype=torch.int32, device=dev),
+           "loss_sum": torch.zeros(1, device=dev)}
+    total = out["loss_sum"]
 
-    # the timed loop calls the C ABI directly (pointers bound once): the HIP events below then
-    # bracket exactly one kernel launch, and no Python wrapper work sits between launches
+    # correctness/status check once through the full Python mirror, outside the timed region
+    r = S.ssnt_fwd_bwd(lt, sl, pl, out=out, check=True, loss_sum=True)
+    assert torch.isfinite(r["loss"]).all()
+    assert torch.isclose(r["loss_sum"], r["loss"].double().sum().float(), rtol=1e-5).all()
+
+    # The timed loop calls the C ABI directly (pointers bound once). N=1: the K steps are one
+    # HIP graph of K kernel launches, replayed with one call (the host issues nothing per step).
+    # N>1: eager launches; each step's loss sum is all-reduced by RCCL asynchronously into one of
+    # two alternating buffers, so the collective overlaps the next step's kernel.
     import ctypes
     lib = S.load()
     wsb = int(lib.ssnt_fwd_bwd_workspace_size(B, T, U))
+    # in-launch loss-sum state: zeroed once, then maintained by the library
+    sum_state = torch.zeros(int(lib.ssnt_fwd_bwd_sum_state_size(B)), dtype=torch.uint8, device=dev)
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
     vp = ctypes.c_void_p
-    cargs = (vp(lt.data_ptr()), None, vp(sl.data_ptr()), vp(pl.data_ptr()), B, T, U, 1,
-             vp(out["loss"].data_ptr()), vp(out["grad"].data_ptr()), None, None, None,
-             vp(ws.data_ptr()) if wsb else None, wsb, None,
-             vp(torch.cuda.current_stream(dev).cuda_stream))
+    totals = [total, torch.zeros(1, device=dev)]
 
-    def launch():
-        rc = lib.ssnt_fwd_bwd_device(*cargs)
+    def cargs_for(stream, tot):
+        return (vp(lt.data_ptr()), None, vp(sl.data_ptr()), vp(pl.data_ptr()), B, T, U, 1,
+                vp(out["loss"].data_ptr()), vp(out["grad"].data_ptr()), None, None, None,
+                vp(ws.data_ptr()) if wsb else None, wsb, None, vp(tot.data_ptr()),
+                vp(sum_state.data_ptr()), vp(stream.cuda_stream))
+
+    def launch(cargs):
+        rc = lib.ssnt_fwd_bwd_sum_device(*cargs)
         if rc != 0:
-            raise RuntimeError(f"ssnt_fwd_bwd_device: {S.status_string(rc)}")
+            raise RuntimeError(f"ssnt_fwd_bwd_sum_device: {S.status_string(rc)}")
 
-    def step():
-        launch()
-        torch.sum(out["loss"], dim=0, keepdim=True, out=total)
-        if dist:
-            torch.distributed.all_reduce(total)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
+    main = torch.cuda.current_stream(dev)
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    if dist:
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if not dist:
+        a_main = cargs_for(main, total)
+        for _ in range(args.warmup):
+            launch(a_main)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(dev)
+        with torch.cuda.graph(graph, stream=cap):
+            a_cap = cargs_for(cap, total)
+            for _ in range(K):
+                launch(a_cap)
+        graph.replay()  # first replay uploads the graph (untimed)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(main)
+        graph.replay()
+        e1.record(main)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    else:
+        a_alt = [cargs_for(main, t) for t in totals]
+        works = []
+
+        def step(i):
+            if i >= 2:
+                works[i - 2].wait()  # stream-side: buffer i%2 is free again
+            launch(a_alt[i % 2])
+            works.append(torch.distributed.all_reduce(totals[i % 2], async_op=True))
+
+        for i in range(args.warmup):
+            step(i)
+        for w in works:
+            w.wait()
+        works.clear()
+        torch.cuda.synchronize()
         torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(K):
-        ev[i][0].record()
-        launch()
-        ev[i][1].record()
-        torch.sum(out["loss"], dim=0, keepdim=True, out=total)
-        if dist:
-            torch.distributed.all_reduce(total)
-    torch.cuda.synchronize()
-    if dist:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(main)
+        for i in range(K):
+            step(i)
+        for w in works:
+            w.wait()
+        e1.record(main)
+        torch.cuda.synchronize()
         torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        elapsed = time.perf_counter() - t0
+    # average kernel duration: the launch stream's events over the K back-to-back launches
+    kern_ms = e0.elapsed_time(e1) / K
     if dist:
         t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

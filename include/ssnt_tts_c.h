@@ -133,6 +133,19 @@ int ssnt_fwd_bwd_device(const float *log_trans, const float *log_obs, const int 
                         float *loss, float *grad_trans, float *grad_obs, float *log_alpha,
                         float *log_beta, void *workspace, size_t workspace_bytes, int *status,
                         void *stream);
+/* As ssnt_fwd_bwd_device, plus the batch loss sum *loss_sum = sum_b loss[b] (device float) in a
+ * fixed summation order (deterministic; independent of the kernel variant). `sum_state` is a
+ * device buffer of ssnt_fwd_bwd_sum_state_size(batch) bytes, zeroed once before its first use
+ * and then left to the library: with it, workgroup 0 forms the sum inside the same launch from
+ * per-utterance 8-byte {tag, loss} granules; NULL costs one extra single-wave launch. One state
+ * per stream of concurrent calls. New: the reference has no forward-backward (SURVEY.md 8(a)
+ * A11). */
+size_t ssnt_fwd_bwd_sum_state_size(int batch);
+int ssnt_fwd_bwd_sum_device(const float *log_trans, const float *log_obs, const int *step_len,
+                            const int *pos_len, int batch, int max_steps, int max_pos, int flags,
+                            float *loss, float *grad_trans, float *grad_obs, float *log_alpha,
+                            float *log_beta, void *workspace, size_t workspace_bytes, int *status,
+                            float *loss_sum, void *sum_state, void *stream);
 /* Host-pointer variant (synchronous; copies through the calling thread's GPU context). */
 int ssnt_fwd_bwd(const float *log_trans, const float *log_obs, const int *step_len,
                  const int *pos_len, int batch, int max_steps, int max_pos, int flags,

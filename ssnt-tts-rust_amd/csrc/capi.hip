@@ -460,6 +460,8 @@ int ssnt_fwd_bwd_set_variant(int variant) { return set_fwd_bwd_variant(variant);
 int ssnt_diag_read(void* host, size_t bytes) { return diag_read(host, bytes); }
 
 
+size_t ssnt_fwd_bwd_sum_state_size(int batch) { return batch > 0 ? fwd_bwd_sum_state_bytes(batch) : 0; }
+
 size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos) {
   if (batch <= 0 || max_steps <= 0 || max_pos <= 0) return 0;
   return fwd_bwd_workspace_bytes(batch, max_steps, max_pos);
@@ -476,6 +478,22 @@ int ssnt_fwd_bwd_device(const float* log_trans, const float* log_obs, const int*
   a.loss = loss; a.grad = grad_trans; a.grad_obs = grad_obs;
   a.log_alpha = log_alpha; a.log_beta = log_beta;
   a.workspace = workspace; a.workspace_bytes = workspace_bytes; a.status = status;
+  return launch_fwd_bwd(a, as_stream(stream));
+}
+
+int ssnt_fwd_bwd_sum_device(const float* log_trans, const float* log_obs, const int* step_len,
+                            const int* pos_len, int batch, int max_steps, int max_pos, int flags,
+                            float* loss, float* grad_trans, float* grad_obs, float* log_alpha,
+                            float* log_beta, void* workspace, size_t workspace_bytes, int* status,
+                            float* loss_sum, void* sum_state, void* stream) {
+  if (!loss_sum) return SSNT_ERR_INVALID_ARG;
+  FwdBwdArgs a{};
+  a.log_trans = log_trans; a.log_obs = log_obs; a.step_len = step_len; a.pos_len = pos_len;
+  a.B = batch; a.T = max_steps; a.U = max_pos; a.flags = flags;
+  a.loss = loss; a.grad = grad_trans; a.grad_obs = grad_obs;
+  a.log_alpha = log_alpha; a.log_beta = log_beta;
+  a.workspace = workspace; a.workspace_bytes = workspace_bytes; a.status = status;
+  a.loss_sum = loss_sum; a.sum_state = sum_state;
   return launch_fwd_bwd(a, as_stream(stream));
 }
 

@@ -340,34 +340,60 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
 }
 
 int set_fwd_bwd_variant(int v) {
-  // 0 stream, 1 two-wave; 2..6: stream with another wave mix (tuning only)
-  if (v < 0 || v > 6) return SSNT_ERR_INVALID_ARG;
+  // 0 stream, 1 two-wave; 2..7: stream with another wave mix (tuning only)
+  if (v < 0 || v > 7) return SSNT_ERR_INVALID_ARG;
   g_variant = v >= 2 ? 0 : v;
   set_stream_mix(v >= 2 ? v - 1 : 0);
   return SSNT_OK;
 }
 
-int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t st) {
-  if (a.B < 0 || a.T <= 0 || a.U <= 0 || !a.log_trans || !a.step_len || !a.pos_len || !a.loss)
-    return SSNT_ERR_INVALID_ARG;
-  if (a.grad_obs && !a.log_obs) return SSNT_ERR_INVALID_ARG;
-  if (a.B == 0) return SSNT_OK;
+namespace {
+__global__ __launch_bounds__(64) void k_loss_sum(const float* loss, int B, float* out) {
+  const float sum = wave_loss_sum(loss, B);
+  if (threadIdx.x == 0) *out = sum;
+}
+
+int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
+  summed = false;
   if (g_variant < 0) {
     const char* e = getenv("SSNT_FWD_BWD_KERNEL");
     g_variant = (e && strcmp(e, "simple") == 0) ? 1 : 0;
   }
   if (g_variant == 0) {
-#ifdef SSNT_EXP
     FwdBwdArgs x = a;
+#ifdef SSNT_EXP
     const char* ee = getenv("SSNT_EXP");
     x.exp = ee ? atoi(ee) : 0;
-    const int rc = launch_fwd_bwd_stream(x, st);
-#else
-    const int rc = launch_fwd_bwd_stream(a, st);
 #endif
+    if (!a.sum_state) x.loss_sum = nullptr;
+    const int rc = launch_fwd_bwd_stream(x, st);
+    summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;
+    summed = false;
   }
-  return a.log_obs ? launch_simple<true>(a, st) : launch_simple<false>(a, st);
+  FwdBwdArgs x = a;
+  x.loss_sum = nullptr;  // the two-wave kernel only writes loss[]
+  return a.log_obs ? launch_simple<true>(x, st) : launch_simple<false>(x, st);
+}
+}  // namespace
+
+size_t fwd_bwd_sum_state_bytes(int B) { return kSumGranuleOffset + 8 * (size_t)(B > 0 ? B : 0); }
+
+int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t st) {
+  if (a.B < 0 || a.T <= 0 || a.U <= 0 || !a.log_trans || !a.step_len || !a.pos_len || !a.loss)
+    return SSNT_ERR_INVALID_ARG;
+  if (a.grad_obs && !a.log_obs) return SSNT_ERR_INVALID_ARG;
+  if (a.B == 0) {
+    if (a.loss_sum) return hipMemsetAsync(a.loss_sum, 0, sizeof(float), st) == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
+    return SSNT_OK;
+  }
+  // batch loss sum: inside the streaming kernel when the caller gives a sum state, else one
+  // extra single-wave pass over loss[] (same fixed order, same bits)
+  bool summed = false;
+  const int rc = launch_variant(a, st, summed);
+  if (rc != SSNT_OK || !a.loss_sum || summed) return rc;
+  hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(64), 0, st, a.loss, a.B, a.loss_sum);
+  return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
 }  // namespace ssnt

@@ -249,7 +249,7 @@ __device__ __forceinline__ void lds_xrow_st(xf* p, const XRow<K>& r) {
   st_vec<2 * K>(reinterpret_cast<float*>(p), v);
 }
 
-template <int K, bool OBS, bool LDS, int kNC, int kNH>
+template <int K, bool OBS, bool LDS, int kNC, int kNH, bool kNoSleep>
 __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream(FwdBwdArgs a) {
   constexpr int kWaves = 2 + 2 * kNC + 2 * kNH;
   constexpr int R = in_slots<OBS>();
@@ -305,7 +305,11 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     if ((S > T || P > U || S < 0 || P < 0) && a.status && threadIdx.x == 0)
       atomicOr(a.status, kStatusBadLength);
     fill_rows(0, wave, kWaves);
-    if (threadIdx.x == 0) a.loss[b] = inf_loss;
+    if (wave == 0) {
+      const unsigned tag = a.loss_sum ? __builtin_amdgcn_readfirstlane(sum_tag(a)) : 0u;
+      if (lane == 0) publish_loss(a, b, inf_loss, tag);
+      if (a.loss_sum && b == 0) finish_loss_sum(a, tag);
+    }
     return;
   }
   const int M = (S - 1) >> 1;
@@ -371,6 +375,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     };
     // ---- Z at the cut: tree-sum over p of alpha[M][p] * beta[M][p] (fixed order, = oracle)
     if (d == 0 && h == 0) {
+      const unsigned tag = a.loss_sum ? sum_tag(a) : 0u;  // (load in flight while waiting)
       spin_until<true>([&] { return ctr_acq(&ctl->a_ready); }, 1, a.status, dg);
       spin_until<true>([&] { return ctr_acq(&ctl->bm_ready); }, 1, a.status, dg);
       const XRow<K> Am = row_ld(M);
@@ -400,7 +405,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       }
       if (lane == 0) {
         ctl->z = z;
-        a.loss[b] = (z.m == 0.0f) ? inf_loss : 0.0f - xf_log(z);
+        publish_loss(a, b, (z.m == 0.0f) ? inf_loss : 0.0f - xf_log(z), tag);
       }
       ctr_rel(&ctl->z_ready, 1);
     } else {
@@ -426,7 +431,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     auto wait_chain = [&](int i) {
       const int need = need_of(i);
       if (chain_seen < need)
-        chain_seen = spin_until<true>([&] { return ctr_ld(&ctl->chain[d]); }, need, a.status, dg);
+        chain_seen = spin_until<!kNoSleep>([&] { return ctr_ld(&ctl->chain[d]); }, need, a.status, dg);
       cbar();
     };
     auto fetch = [&](int i, GIn& in) {
@@ -558,6 +563,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     const int d = (wave - 2) & 1;
     const int c = (wave - 2) >> 1;
     constexpr int D = conv_depth<K>();
+    const unsigned tag0 = (d == 0 && c == 0 && b == 0 && a.loss_sum) ? sum_tag(a) : 0u;
     const int chain_end = d == 0 ? S - 1 : S;
     unsigned char* ring = inr + (size_t)d * R * slot_bytes;
     auto load = [&](int r, Item<K, OBS>& it) {
@@ -615,9 +621,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           if (q >= 0 && !EXP(7)) {
             const int need_c = min(q + 1, chain_end);
             if (seen_chain < need_c)
-              seen_chain = spin_until<true>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
+              seen_chain = spin_until<!kNoSleep>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
             if (q >= hb && seen_grad <= q)
-              seen_grad = spin_until<true>([&] { return first_missing<kNH>(ctl->help[d], hb); }, q + 1, a.status, dg);
+              seen_grad = spin_until<!kNoSleep>([&] { return first_missing<kNH>(ctl->help[d], hb); }, q + 1, a.status, dg);
           }
           cbar();
           unsigned char* sl = ring + (size_t)(r % R) * slot_bytes;
@@ -651,6 +657,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     }
     dg.flush(b, wave);
     fill_rows(S, d * kNC + c, 2 * kNC);  // zero the rows beyond S
+    // workgroup 0 forms the batch loss sum once every utterance has published its loss (all
+    // did so at their cut, long before this converter runs out of rows)
+    if (d == 0 && c == 0 && b == 0 && a.loss_sum && !EXP(7)) finish_loss_sum(a, tag0);
     return;
   }
 
@@ -859,9 +868,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-template <int K, bool OBS, bool LDS, int NC, int NH>
+template <int K, bool OBS, bool LDS, int NC, int NH, bool NS>
 int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
-  auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH>;
+  auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH, NS>;
   if (lds > 64 * 1024) {  // dynamic LDS above 64 KiB needs the attribute (idempotent)
     static bool attr_set = false;
     if (!attr_set) {
@@ -874,7 +883,7 @@ int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
-template <int K, bool OBS, int NC, int NH>
+template <int K, bool OBS, int NC, int NH, bool NS = false>
 int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
   // whole lane slices and 16-byte aligned tensors (the kernel's vector accesses)
   const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
@@ -887,20 +896,22 @@ int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
   const bool lds = head + rows <= kLdsBudget;
   if (!lds && (a.workspace == nullptr || a.workspace_bytes < (size_t)a.B * rows))
     return SSNT_ERR_WORKSPACE;
-  return lds ? launch_stream_kernel<K, OBS, true, NC, NH>(a, head + rows, st)
-             : launch_stream_kernel<K, OBS, false, NC, NH>(a, head, st);
+  return lds ? launch_stream_kernel<K, OBS, true, NC, NH, NS>(a, head + rows, st)
+             : launch_stream_kernel<K, OBS, false, NC, NH, NS>(a, head, st);
 }
 
-template <bool OBS, int NC, int NH>
+template <bool OBS>
 int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
+  // wave mix per lane width: 16 waves (3 converters + 4 gradient waves per direction) while a
+  // wave fits 128 VGPRs (K <= 2); 10 waves for K >= 4 (168 VGPRs, no spills)
 #ifdef SSNT_EXP
   if (OBS || a.U <= 64 || a.U > 128) return SSNT_ERR_UNSUPPORTED;
-  return launch_stream_k<2, false, NC, NH>(a, st);
+  return launch_stream_k<2, false, 3, 4>(a, st);
 #else
-  if (a.U <= 64) return launch_stream_k<1, OBS, NC, NH>(a, st);
-  if (a.U <= 128) return launch_stream_k<2, OBS, NC, NH>(a, st);
-  if (a.U <= 256) return launch_stream_k<4, OBS, NC, NH>(a, st);
-  if (a.U <= 512) return launch_stream_k<8, OBS, NC, NH>(a, st);
+  if (a.U <= 64) return launch_stream_k<1, OBS, 3, 4>(a, st);
+  if (a.U <= 128) return launch_stream_k<2, OBS, 3, 4>(a, st);
+  if (a.U <= 256) return launch_stream_k<4, OBS, 2, 2>(a, st);
+  if (a.U <= 512) return launch_stream_k<8, OBS, 2, 2>(a, st);
   return SSNT_ERR_UNSUPPORTED;
 #endif
 }
@@ -938,10 +949,11 @@ int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
       case 3: return launch_stream_k<2, false, 2, 4>(a, st);
       case 4: return launch_stream_k<2, false, 2, 2>(a, st);
       case 5: return launch_stream_k<2, false, 2, 3>(a, st);
+      case 6: return launch_stream_k<2, false, 3, 3>(a, st);
       default: break;
     }
   }
-  return a.log_obs ? launch_stream_obs<true, 3, 3>(a, st) : launch_stream_obs<false, 3, 3>(a, st);
+  return a.log_obs ? launch_stream_obs<true>(a, st) : launch_stream_obs<false>(a, st);
 }
 
 void set_stream_mix(int m) { g_mix = m; }

@@ -374,6 +374,66 @@ __device__ __forceinline__ void buf_st(const float* v, __amdgpu_buffer_rsrc_t r,
   }
 }
 
+// Batch loss sum inside the launch (ssnt_fwd_bwd_sum_device). Utterance b publishes
+// {tag, loss bits} as ONE 8-byte write-through granule (MI355X hand-off form R2: the data is the
+// flag -- no fence, no read-modify-write atomic, nothing for 256 workgroups to serialise on).
+// Workgroup 0 re-reads the B granules until every tag is this launch's, sums them in a fixed
+// order (64 lane-strided partial sums, then an xor butterfly: f32 addition is commutative, so
+// every lane ends with the same bits) and advances the epoch word. State layout: u32 epoch at
+// byte 0, granule b at byte 64 + 8b; all zero before the first call.
+constexpr size_t kSumGranuleOffset = 64;
+__device__ __forceinline__ unsigned long long* sum_granule(const FwdBwdArgs& a, int b) {
+  return reinterpret_cast<unsigned long long*>(reinterpret_cast<unsigned char*>(a.sum_state) +
+                                               kSumGranuleOffset) + b;
+}
+// this launch's tag: epoch + 1 (the epoch only advances after every workgroup has published)
+__device__ __forceinline__ unsigned sum_tag(const FwdBwdArgs& a) {
+  return __hip_atomic_load(reinterpret_cast<unsigned*>(a.sum_state), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+// one lane: loss[b] = v, and the granule when a batch sum is requested
+__device__ __forceinline__ void publish_loss(const FwdBwdArgs& a, int b, float v, unsigned tag) {
+  a.loss[b] = v;
+  if (a.loss_sum)
+    __hip_atomic_store(sum_granule(a, b),
+                       ((unsigned long long)tag << 32) | __builtin_bit_cast(unsigned, v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one wave of workgroup 0: wait for every granule of this launch, write the sum, advance epoch
+__device__ __forceinline__ void finish_loss_sum(const FwdBwdArgs& a, unsigned tag) {
+  const int lane = threadIdx.x & 63;
+  for (int spins = 0;; ++spins) {
+    bool ok = true;
+    for (int i = lane; i < a.B; i += 64)
+      ok &= (unsigned)(__hip_atomic_load(sum_granule(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
+    if (__all(ok)) break;
+    if (spins > (1 << 20)) {  // bounded: report and give up (the sum is then not written)
+      if (lane == 0 && a.status) atomicOr(a.status, kStatusTimeout);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  float acc = 0.0f;
+  for (int i = lane; i < a.B; i += 64)
+    acc += __builtin_bit_cast(float, (unsigned)__hip_atomic_load(sum_granule(a, i), __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) {
+    *a.loss_sum = acc;
+    __hip_atomic_store(reinterpret_cast<unsigned*>(a.sum_state), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// the same fixed order over a finished loss[] (the separate pass when no state is given)
+__device__ __forceinline__ float wave_loss_sum(const float* loss, int B) {
+  const int lane = threadIdx.x & 63;
+  float acc = 0.0f;
+  for (int i = lane; i < B; i += 64) acc += loss[i];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+  return acc;
+}
+
 template <int K>
 __device__ __forceinline__ void xrow_pack(const XRow<K>& r, float* v) {
 #pragma unroll

@@ -33,9 +33,12 @@ struct FwdBwdArgs {
   void* workspace;   // row storage when the rows do not fit LDS
   size_t workspace_bytes;
   int* status;  // device status word or null
+  float* loss_sum;   // fixed-order sum of loss[0..B) or null
+  void* sum_state;   // in-launch sum state (lattice_dev.h; zero before the first call) or null
   int exp;      // experiment knobs (SSNT_EXP builds only; 0 in the product)
 };
 size_t fwd_bwd_workspace_bytes(int B, int T, int U);
+size_t fwd_bwd_sum_state_bytes(int B);  // 64 + 8 B
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
 int set_fwd_bwd_variant(int v);
 // streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take

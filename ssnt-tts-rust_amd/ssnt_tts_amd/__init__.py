@@ -256,8 +256,23 @@ def _workspace(dev, nbytes):
     return buf
 
 
+_sum_states = {}
+
+
+def _sum_state(dev, B):
+    """Zeroed in-launch loss-sum state (ssnt_fwd_bwd_sum_state_size), one per (device, stream)."""
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    nbytes = int(load().ssnt_fwd_bwd_sum_state_size(B))
+    t = _sum_states.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+        _sum_states[key] = t
+    return t
+
+
 def ssnt_fwd_bwd(log_trans, step_len, pos_len, log_obs=None, *, terminal_emit=True,
-                 zero_infinity=False, need_grad=True, debug=False, check=False, out=None):
+                 zero_infinity=False, need_grad=True, debug=False, check=False, out=None,
+                 loss_sum=False):
     """Forward-backward over the emit/shift lattice.
 
     log_trans (B,T,U,2) f32 [emit, shift] natural-log probabilities; step_len / pos_len (B,)
@@ -265,6 +280,8 @@ def ssnt_fwd_bwd(log_trans, step_len, pos_len, log_obs=None, *, terminal_emit=Tr
     ``loss`` (B,) = -ln Z, ``grad`` (B,T,U,2) = d loss / d log_trans (if need_grad),
     ``grad_obs`` (if log_obs given and need_grad), ``log_alpha`` / ``log_beta`` (if debug).
     ``out`` may pass preallocated tensors under the same keys (reused, for benchmarking).
+    ``loss_sum=True`` adds ``loss_sum`` (1,) = sum_b loss[b], formed inside the same launch in a
+    fixed order (ssnt_fwd_bwd_sum_device).
     """
     lib = load(require_gpu=True)
     lt = _dev(log_trans, torch.float32, "log_trans")
@@ -300,10 +317,19 @@ def ssnt_fwd_bwd(log_trans, step_len, pos_len, log_obs=None, *, terminal_emit=Tr
         st = _status(dev)
     else:
         st.zero_()
-    rc = lib.ssnt_fwd_bwd_device(_p(lt), _p(lo), _p(sl), _p(pl), B, T, U, flags, _p(loss), _p(grad),
-                                 _p(gobs), _p(la), _p(lb), _p(ws), wsb, _p(st), _stream(dev))
+    if loss_sum:
+        lsum = _buf("loss_sum", (1,), True)
+        rc = lib.ssnt_fwd_bwd_sum_device(_p(lt), _p(lo), _p(sl), _p(pl), B, T, U, flags, _p(loss),
+                                         _p(grad), _p(gobs), _p(la), _p(lb), _p(ws), wsb, _p(st),
+                                         _p(lsum), _p(_sum_state(dev, B)), _stream(dev))
+    else:
+        rc = lib.ssnt_fwd_bwd_device(_p(lt), _p(lo), _p(sl), _p(pl), B, T, U, flags, _p(loss),
+                                     _p(grad), _p(gobs), _p(la), _p(lb), _p(ws), wsb, _p(st),
+                                     _stream(dev))
     _finish("ssnt_fwd_bwd", rc, st, check)
     res = {"loss": loss, "status": st}
+    if loss_sum:
+        res["loss_sum"] = lsum
     if grad is not None:
         res["grad"] = grad
     if gobs is not None:

@@ -34,9 +34,12 @@ SIGNATURES = {
     "ssnt_status_from_bits": (c_int, [c_int]),
     "ssnt_version": (c_int, [ctypes.c_char_p, c_size_t]),
     "ssnt_fwd_bwd_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "ssnt_fwd_bwd_sum_state_size": (c_size_t, [c_int]),
     "ssnt_fwd_bwd_set_variant": (c_int, [c_int]),
     "ssnt_fwd_bwd_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
                                     c_size_t, P, P]),
+    "ssnt_fwd_bwd_sum_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
+                                        c_size_t, P, P, P, P]),
     "ssnt_fwd_bwd": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "ssnt_beam_search_decode_device": (c_int, [P, P, P, P, P, P, c_int, c_int, P, P, P, P, P, P,
                                                P, P]),

@@ -152,9 +152,9 @@ def test_autograd_function(gpu, oracle):
     assert np.array_equal(x.grad.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7])
 def test_tuning_wave_mixes_bit_exact(gpu, oracle, kernel_variant, variant):
-    # the converter / gradient wave mixes of the streaming kernel (ssnt_fwd_bwd_set_variant 2..6,
+    # the converter / gradient wave mixes of the streaming kernel (ssnt_fwd_bwd_set_variant 2..7,
     # K = 2 shapes) must be bit-identical to the oracle like the default mix
     if kernel_variant != 0:
         pytest.skip("mix variants are streaming-kernel variants")
@@ -169,3 +169,54 @@ def test_tuning_wave_mixes_bit_exact(gpu, oracle, kernel_variant, variant):
     g = _run_gpu(gpu, lt, S, P)
     o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
     _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+
+
+def _wave_order_sum(loss):
+    """The library's fixed summation order: 64 lane-strided f32 partial sums, then an xor
+    butterfly (lattice_dev.h wave_loss_sum)."""
+    acc = np.zeros(64, np.float32)
+    for i, v in enumerate(np.asarray(loss, np.float32)):
+        acc[i % 64] = np.float32(acc[i % 64] + v)
+    off = 32
+    while off >= 1:
+        acc = (acc + acc[np.arange(64) ^ off]).astype(np.float32)
+        off //= 2
+    return acc[0]
+
+
+@pytest.mark.parametrize("B", [1, 70, 256])
+def test_fused_loss_sum(gpu, oracle, kernel_variant, B):
+    # ssnt_fwd_bwd_sum_device: batch loss sum in the same launch (last workgroup), fixed order,
+    # counter re-armed for the next call; infeasible utterances (+inf) included
+    dev = torch.device("cuda:0")
+    T, U = 40, 24
+    rng = np.random.default_rng(B)
+    lt = oracle.synth_log_trans(B, T, U, seed=B)
+    P = rng.integers(1, U + 1, size=B)
+    S = np.array([rng.integers(max(1, p), T + 1) for p in P])
+    if B > 3:
+        S[3], P[3] = 5, 9  # infeasible: loss 0 with zero_infinity
+    o = oracle.fwd_bwd_xf(lt, S, P, flags=F_TERM | F_ZINF)
+    want = _wave_order_sum(o["loss"])
+    x = torch.from_numpy(lt).to(dev)
+    sl = torch.tensor(S, dtype=torch.int32, device=dev)
+    pl = torch.tensor(P, dtype=torch.int32, device=dev)
+    for _ in range(3):  # the counter must re-arm itself between calls
+        r = gpu.ssnt_fwd_bwd(x, sl, pl, zero_infinity=True, loss_sum=True, check=True)
+        assert np.array_equal(r["loss"].cpu().numpy(), o["loss"])
+        assert r["loss_sum"].cpu().numpy()[0] == want
+    # without a counter: one extra single-wave pass, same bits
+    lib = gpu.load()
+    loss = torch.empty(B, device=dev)
+    grad = torch.empty((B, T, U, 2), device=dev)
+    lsum = torch.full((1,), -1.0, device=dev)
+    import ctypes
+    vp = ctypes.c_void_p
+    rc = lib.ssnt_fwd_bwd_sum_device(vp(x.data_ptr()), None, vp(sl.data_ptr()), vp(pl.data_ptr()),
+                                     B, T, U, F_TERM | F_ZINF, vp(loss.data_ptr()),
+                                     vp(grad.data_ptr()), None, None, None, None, 0, None,
+                                     vp(lsum.data_ptr()), None,
+                                     vp(torch.cuda.current_stream(dev).cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert lsum.cpu().numpy()[0] == want

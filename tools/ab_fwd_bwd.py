@@ -14,7 +14,7 @@ sys.path.insert(0, str(ROOT / "ssnt-tts-rust_amd"))
 import ssnt_tts_amd as S  # noqa: E402
 
 
-def bench_shape(B, T, U, variants=(0, 1, 2, 3), rounds=5, iters=10):
+def bench_shape(B, T, U, variants=(0, 1, 2, 3), rounds=5, iters=10, use_sum=False):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(0)
@@ -30,14 +30,22 @@ def bench_shape(B, T, U, variants=(0, 1, 2, 3), rounds=5, iters=10):
     st = vp(torch.cuda.current_stream().cuda_stream)
     args = (vp(lt.data_ptr()), None, vp(sl.data_ptr()), vp(pl.data_ptr()), B, T, U, 1,
             vp(loss.data_ptr()), vp(grad.data_ptr()), None, None, None,
-            vp(ws.data_ptr()) if wsb else None, wsb, None, st)
+            vp(ws.data_ptr()) if wsb else None, wsb, None)
+    lsum = torch.zeros(1, device=dev)
+    state = torch.zeros(int(lib.ssnt_fwd_bwd_sum_state_size(B)), dtype=torch.uint8, device=dev)
+    if use_sum:  # fused batch loss sum (ssnt_fwd_bwd_sum_device)
+        args = args + (vp(lsum.data_ptr()), vp(state.data_ptr()), st)
+        call = lib.ssnt_fwd_bwd_sum_device
+    else:
+        args = args + (st,)
+        call = lib.ssnt_fwd_bwd_device
     res = {v: [] for v in variants}
     ref = None
     for rnd in range(rounds):
         for v in variants:
             lib.ssnt_fwd_bwd_set_variant(v)
             for _ in range(2):
-                rc = lib.ssnt_fwd_bwd_device(*args)
+                rc = call(*args)
                 assert rc == 0, f"variant {v}: status {rc}"
             torch.cuda.synchronize()
             if rnd == 0:
@@ -49,7 +57,7 @@ def bench_shape(B, T, U, variants=(0, 1, 2, 3), rounds=5, iters=10):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(iters):
-                lib.ssnt_fwd_bwd_device(*args)
+                call(*args)
             e1.record()
             torch.cuda.synchronize()
             res[v].append(e0.elapsed_time(e1) / iters * 1e3)
