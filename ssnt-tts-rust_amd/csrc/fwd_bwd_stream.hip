@@ -50,6 +50,8 @@ template <bool OBS>
 constexpr int in_slots() { return OBS ? 4 : 8; }  // converted-row ring slots per direction
 template <bool OBS>
 constexpr int out_slots() { return OBS ? 4 : 8; }  // chain-row ring (rows past the cut) per direction
+template <bool OBS>
+constexpr int kChainPrefetch(int R) { return R >= 16 ? 4 : 2; }  // factor rows in flight per chain
 template <int K>
 constexpr int conv_depth() { return K <= 2 ? 8 : (K <= 4 ? 4 : 2); }  // converter prefetch rows
 
@@ -93,6 +95,8 @@ __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 // with ssnt_diag_read() (tools/diag_fwd_bwd.py). g_diag[b][wave][8]: 0 total cycles, 1 cycles
 // spent spinning, 2 spins that waited, 3 cycle of the cut (chains: alpha[M] / beta[M] stored;
 // gradient waves: Z known), 4 cycles spent spinning before the cut. Never present in the product build.
+// (s_memtime is a scalar-memory read: reading it waits lgkmcnt(0), i.e. drains the wave's LDS
+// queue, so stamps inside a loop perturb what they time.)
 #ifdef SSNT_DIAG
 __device__ unsigned long long g_diag[1024][2 + 4 * kMaxW][8];
 struct Diag {
@@ -158,6 +162,43 @@ __device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...
 template <int N, typename F>
 __device__ __forceinline__ void sfor(F&& f) {
   sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Wave roles: chains, converters, gradient waves, in wave order. The hardware places wave w of
+// a workgroup on SIMD (base + w) % 4 (measured, tools/micro/micro_simd.hip), so this order
+// spreads each role over all four SIMDs. (Tried: giving each chain a SIMD shared only with
+// gradient waves -- idle until the cut -- and packing the converters onto the other two SIMDs:
+// the chains ran no faster and the packed converters starved them, 44 -> 48 us. kSimdRoles.)
+constexpr bool kSimdRoles = false;
+struct Role {
+  int kind;  // 0 chain, 1 converter, 2 gradient wave
+  int d;     // direction: 0 forward, 1 backward
+  int idx;   // converter c / gradient wave h within the direction
+  int slot;  // linear index (diagnostics): 0/1 chains, 2+2c+d converters, 2+2kNC+2h+d gradient
+};
+template <int kNC, int kNH>
+__device__ __forceinline__ Role role_of(int w) {
+  constexpr int kW = 2 + 2 * kNC + 2 * kNH;
+  constexpr int n0 = (kW + 3) / 4, n1 = (kW + 2) / 4, n2 = (kW + 1) / 4, n3 = kW / 4;
+  constexpr bool simd_aware = kSimdRoles && n2 >= kNC && n3 >= kNC &&
+                              (n0 - 1) + (n2 - kNC) == kNH && (n1 - 1) + (n3 - kNC) == kNH;
+  Role r;
+  if constexpr (simd_aware) {
+    const int g = w & 3, k = w >> 2;
+    if (g <= 1) {
+      r = k == 0 ? Role{0, g, 0, 0} : Role{2, g, k - 1, 0};
+    } else if (k < kNC) {
+      r = Role{1, g - 2, k, 0};
+    } else {
+      r = Role{2, g - 2, (g == 2 ? n0 - 1 : n1 - 1) + (k - kNC), 0};
+    }
+  } else {
+    if (w < 2) r = Role{0, w, 0, 0};
+    else if (w < 2 + 2 * kNC) r = Role{1, (w - 2) & 1, (w - 2) >> 1, 0};
+    else r = Role{2, (w - 2 - 2 * kNC) & 1, (w - 2 - 2 * kNC) >> 1, 0};
+  }
+  r.slot = r.kind == 0 ? r.d : r.kind == 1 ? 2 + 2 * r.idx + r.d : 2 + 2 * kNC + 2 * r.idx + r.d;
+  return r;
 }
 
 // neighbour moves with zero fill at the wave edge (bound_ctrl): foldable into the consumer
@@ -249,15 +290,16 @@ __device__ __forceinline__ void lds_xrow_st(xf* p, const XRow<K>& r) {
   st_vec<2 * K>(reinterpret_cast<float*>(p), v);
 }
 
-template <int K, bool OBS, bool LDS, int kNC, int kNH, bool kNoSleep>
+template <int K, bool OBS, bool LDS, int kNC, int kNH, int kRingSel>
 __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream(FwdBwdArgs a) {
   constexpr int kWaves = 2 + 2 * kNC + 2 * kNH;
-  constexpr int R = in_slots<OBS>();
+  constexpr int R = kRingSel ? kRingSel : in_slots<OBS>();
   constexpr int kR2 = out_slots<OBS>();
   static_assert(R % kR2 == 0, "ring sizes");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Role role = role_of<kNC, kNH>(wave);
   const int lane = threadIdx.x & 63;
   const int T = a.T, U = a.U;
   const int S = a.step_len[b];
@@ -338,7 +380,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 
   if (threadIdx.x < kCtlBytes / 4) reinterpret_cast<int*>(smem)[threadIdx.x] = 0;
   XRow<K> X = xrow_zero<K>();
-  if (wave == 0) {  // alpha[0]: 1 at p = 0 (x obs[0][0])
+  if (role.kind == 0 && role.d == 0) {  // alpha[0]: 1 at p = 0 (x obs[0][0])
     if (lane == 0) {
       if constexpr (OBS) {
         const xf o = xf_exp(lo[0], true);
@@ -355,11 +397,11 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   __syncthreads();
   Diag dg;
 
-  if (EXP(7) && (wave < 2 || wave >= 2 + 2 * kNC)) return;  // experiment: converters alone
-  if (wave >= 2 + 2 * kNC) {
+  if (EXP(7) && role.kind != 1) return;  // experiment: converters alone
+  if (role.kind == 2) {
     // =============================== gradient waves ======================================
-    const int d = (wave - 2 - 2 * kNC) & 1;
-    const int h = (wave - 2 - 2 * kNC) >> 1;
+    const int d = role.d;
+    const int h = role.idx;
     const int hb = d == 0 ? M : S - M;  // first stream row of this direction's gradient rows
     const int n_rows = d == 0 ? S - M : M;  // transitions M..S-1 / M-1..0
     const int nmine = (n_rows - h + kNH - 1) / kNH;
@@ -431,7 +473,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     auto wait_chain = [&](int i) {
       const int need = need_of(i);
       if (chain_seen < need)
-        chain_seen = spin_until<!kNoSleep>([&] { return ctr_ld(&ctl->chain[d]); }, need, a.status, dg);
+        chain_seen = spin_until<true>([&] { return ctr_ld(&ctl->chain[d]); }, need, a.status, dg);
       cbar();
     };
     auto fetch = [&](int i, GIn& in) {
@@ -554,14 +596,14 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       row(i, gin0, gin1);
       if (i + 1 < nmine) row(i + 1, gin1, gin0);
     }
-    dg.flush(b, wave);
+    dg.flush(b, role.slot);
     return;
   }
 
-  if (wave >= 2) {
+  if (role.kind == 1) {
     // =============================== converters ==========================================
-    const int d = (wave - 2) & 1;
-    const int c = (wave - 2) >> 1;
+    const int d = role.d;
+    const int c = role.idx;
     constexpr int D = conv_depth<K>();
     const unsigned tag0 = (d == 0 && c == 0 && b == 0 && a.loss_sum) ? sum_tag(a) : 0u;
     const int chain_end = d == 0 ? S - 1 : S;
@@ -621,9 +663,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           if (q >= 0 && !EXP(7)) {
             const int need_c = min(q + 1, chain_end);
             if (seen_chain < need_c)
-              seen_chain = spin_until<!kNoSleep>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
+              seen_chain = spin_until<true>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
             if (q >= hb && seen_grad <= q)
-              seen_grad = spin_until<!kNoSleep>([&] { return first_missing<kNH>(ctl->help[d], hb); }, q + 1, a.status, dg);
+              seen_grad = spin_until<true>([&] { return first_missing<kNH>(ctl->help[d], hb); }, q + 1, a.status, dg);
           }
           cbar();
           unsigned char* sl = ring + (size_t)(r % R) * slot_bytes;
@@ -655,7 +697,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         load(c + kNC * (k + D), pf[i]);
       }
     }
-    dg.flush(b, wave);
+    dg.flush(b, role.slot);
     fill_rows(S, d * kNC + c, 2 * kNC);  // zero the rows beyond S
     // workgroup 0 forms the batch loss sum once every utterance has published its loss (all
     // did so at their cut, long before this converter runs out of rows)
@@ -665,11 +707,12 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 
   // ================================== chains =============================================
   // Unrolled blocks of R steps aligned to R (slot offsets are compile-time); blocks that lie
-  // inside one phase run without per-step guards. Factors for row r+2 are read into row r's
-  // register buffer as soon as row r is done, so a full step hides the LDS latency. All LDS
+  // inside one phase run without per-step guards. Factors for row r+PF are read into row r's
+  // register buffer as soon as row r is done, so PF-1 steps hide the LDS latency (PF = 4 was
+  // tried: no faster before the cut, slower after it -- less ring slack). All LDS
   // addresses are per-lane pointers prepared before the loop (lanes past U: junk / clamped).
   __builtin_amdgcn_s_setprio(3);
-  const int d = wave;
+  const int d = role.d;
   int ready = 0;  // stream rows known converted
   auto wait_row = [&](int r) {  // r: a row that exists
     if (r >= ready)
@@ -703,7 +746,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       }
     }
   };
-  XRow<K> Eb[2], Xb[2], Ob[2];
+  constexpr int PF = kChainPrefetch<OBS>(R);  // rows of factors in flight per chain
+  static_assert(R % PF == 0 && PF < R, "prefetch buffers tile the ring");
+  XRow<K> Eb[PF], Xb[PF], Ob[PF];
   // Steps run in half-blocks of H = R/2 (unrolled by R: slot offsets compile-time). All waits
   // -- converted rows up to two past the half-block, ring rows released by the gradient waves --
   // happen at half-block boundaries, so the H steps in between are straight-line code and the
@@ -712,8 +757,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // Phase 2 (past the cut) publishes every H2 steps instead: there the gradient waves read each
   // factor slot right behind the chain and the converters need it back, so the hand-off
   // chain -> gradient waves -> converters -> chain has to close within the ring's slack.
-  using H1 = std::integral_constant<int, R / 2>;
-  using H2 = std::integral_constant<int, (R / 4 > 2 ? R / 4 : 2)>;
+  using H1 = std::integral_constant<int, (R >= 16 ? R / 4 : R / 2)>;
+  using H2 = std::integral_constant<int, (R >= 16 ? R / 8 : (R / 4 > 2 ? R / 4 : 2))>;
   auto run = [&](auto Hc, int lo, int hi, auto&& step, auto&& hwait) {
     constexpr int HS = decltype(Hc)::value;
     static_assert(R % HS == 0, "sub-blocks tile the ring");
@@ -733,7 +778,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         }
         cbar();
         ctr_st(&ctl->chain[d], min(hb0 + HS, hi));
-        ctr_st(&ctl->sread[d], min(hb0 + HS, hi) + 2);  // slot reads run two rows ahead
+        ctr_st(&ctl->sread[d], min(hb0 + HS, hi) + PF);  // slot reads run PF rows ahead
       });
     }
   };
@@ -741,10 +786,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     // ---------------- alpha chain: stream row r = transition r -> alpha[r+1] --------------
     const int n = S - 1;
     const int last = max(n - 1, 0);  // last stream row the chain reads
-    wait_row(min(1, last));
+    wait_row(min(PF - 1, last));
     cbar();
-    rd(0, Eb[0], Xb[0], Ob[0]);
-    rd(1 % R, Eb[1], Xb[1], Ob[1]);
+    sfor<PF>([&](auto J) { rd(decltype(J)::value, Eb[decltype(J)::value], Xb[decltype(J)::value], Ob[decltype(J)::value]); });
     int help_seen = M + 1;  // first alpha ring row not yet released by the gradient waves
     // storage write pointer for alpha[r+1] (LDS mode)
     xf* wp = act ? rows + (size_t)U + p0 : reinterpret_cast<xf*>(junk_lane);
@@ -752,7 +796,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     // steps [r0, r1): rows up to r1+1 converted; phase 2: ring rows up to r1-kR2 released
     auto hwait = [&](int r0, int r1, bool phase2) {
       (void)r0;
-      wait_row(min(r1 + 1, last));
+      wait_row(min(r1 - 1 + PF, last));
       if (phase2) {
         const int q = r1 - kR2;  // newest previous occupant the half-block overwrites
         if (q > M && help_seen <= q)
@@ -762,7 +806,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     };
     auto step = [&](auto Ic, int base, bool live, auto Ph) {
       constexpr int i = decltype(Ic)::value;
-      constexpr int par = i & 1;
+      constexpr int par = i % PF;
       constexpr bool phase2 = decltype(Ph)::value;
       if (!live) return;
       const int r = base + i;
@@ -777,10 +821,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       } else {
         lds_xrow_st<K>(optr[(i + 1) % kR2], X);
       }
-      rd((i + 2) % R, Eb[par], Xb[par], Ob[par]);  // row r+2 (a stale slot past the end is dropped)
+      rd((i + PF) % R, Eb[par], Xb[par], Ob[par]);  // row r+PF (a stale slot past the end is dropped)
     };
     if (M == 0) ctr_rel(&ctl->a_ready, 1);
-    ctr_st(&ctl->sread[0], 2);  // slots of rows 0, 1 have been read
+    ctr_st(&ctl->sread[0], PF);  // slots of rows 0..PF-1 have been read
     run(H1{}, 0, M, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::false_type{}); },
         [&](int r0, int r1) { hwait(r0, r1, false); });
     if (M > 0) {
@@ -795,10 +839,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     // beta rows past the cut (s < M) go to ring row r % kR2 (r = S-1-s)
     const int c = S - 1 - M;  // stream row of the cut (beta[M])
     const int last = S - 1;
-    wait_row(min(2, last));
+    wait_row(min(PF, last));
     cbar();
-    rd(0, Eb[0], Xb[0], Ob[0]);
-    rd(1 % R, Eb[1], Xb[1], Ob[1]);
+    sfor<PF>([&](auto J) { rd(decltype(J)::value, Eb[decltype(J)::value], Xb[decltype(J)::value], Ob[decltype(J)::value]); });
     int help_seen = S - M;  // first beta gradient row (stream rows) not finished
     xf* wp = act ? rows + (size_t)(S - 1) * U + p0 : reinterpret_cast<xf*>(junk_lane);  // beta[S-1-r]
     const int wstep = act ? U : 0;
@@ -823,7 +866,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     };
     auto hwait = [&](int r0, int r1, bool ring) {
       (void)r0;
-      wait_row(min(r1 + 1, last));
+      wait_row(min(r1 - 1 + PF, last));
       if (ring) {
         // previous occupants: stream rows up to r1-1-kR2, read by gradient rows q and q+1
         const int q = r1 - 1 - kR2;
@@ -842,19 +885,19 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     if (c == 0) put(0, 0, std::integral_constant<int, 1>{});
     else put(0, 0, std::integral_constant<int, 0>{});
     cbar();
-    rd(2 % R, Eb[0], Xb[0], Ob[0]);
+    rd(PF % R, Eb[0], Xb[0], Ob[0]);
     auto step = [&](auto Ic, int base, bool live, auto Kd) {
       constexpr int i = decltype(Ic)::value;
-      constexpr int par = i & 1;
+      constexpr int par = i % PF;
       if (!live) return;
       const int r = base + i;
       beta_chain<K, OBS>(X, Eb[par], Xb[par], Ob[par]);
       put(r, i, Kd);
-      rd((i + 2) % R, Eb[par], Xb[par], Ob[par]);
+      rd((i + PF) % R, Eb[par], Xb[par], Ob[par]);
     };
     cbar();
     ctr_st(&ctl->chain[1], 1);  // stream row 0 (the terminal row) is done
-    ctr_st(&ctl->sread[1], 3);  // slots of rows 0..2 have been read
+    ctr_st(&ctl->sread[1], PF + 1);  // slots of rows 0..PF have been read
     run(H1{}, 1, c, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 0>{}); },
         [&](int r0, int r1) { hwait(r0, r1, false); });
     if (c >= 1)
@@ -863,14 +906,14 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     run(H2{}, c + 1, S, [&](auto Ic, int base, bool live) { step(Ic, base, live, std::integral_constant<int, 2>{}); },
         [&](int r0, int r1) { hwait(r0, r1, true); });
   }
-  dg.flush(b, wave);
+  dg.flush(b, role.slot);
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-template <int K, bool OBS, bool LDS, int NC, int NH, bool NS>
+template <int K, bool OBS, bool LDS, int NC, int NH, int RS>
 int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
-  auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH, NS>;
+  auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH, RS>;
   if (lds > 64 * 1024) {  // dynamic LDS above 64 KiB needs the attribute (idempotent)
     static bool attr_set = false;
     if (!attr_set) {
@@ -883,21 +926,21 @@ int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
-template <int K, bool OBS, int NC, int NH, bool NS = false>
+template <int K, bool OBS, int NC, int NH, int RS = 0>
 int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
   // whole lane slices and 16-byte aligned tensors (the kernel's vector accesses)
   const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
                    aligned16(a.grad) && aligned16(a.grad_obs) && aligned16(a.log_alpha) &&
                    aligned16(a.log_beta) && aligned16(a.workspace);
   if (!vec) return SSNT_ERR_UNSUPPORTED;
-  const size_t head = stream_head_bytes(K, a.U, OBS);
+  const size_t head = stream_head_bytes(K, a.U, OBS, RS);
   if (head > kLdsBudget) return SSNT_ERR_UNSUPPORTED;
   const size_t rows = (size_t)a.T * a.U * sizeof(xf);
   const bool lds = head + rows <= kLdsBudget;
   if (!lds && (a.workspace == nullptr || a.workspace_bytes < (size_t)a.B * rows))
     return SSNT_ERR_WORKSPACE;
-  return lds ? launch_stream_kernel<K, OBS, true, NC, NH, NS>(a, head + rows, st)
-             : launch_stream_kernel<K, OBS, false, NC, NH, NS>(a, head, st);
+  return lds ? launch_stream_kernel<K, OBS, true, NC, NH, RS>(a, head + rows, st)
+             : launch_stream_kernel<K, OBS, false, NC, NH, RS>(a, head, st);
 }
 
 template <bool OBS>
@@ -930,8 +973,8 @@ int diag_read(void* host, size_t bytes) {
 #endif
 }
 
-size_t stream_head_bytes(int K, int U, bool obs) {
-  const int R = obs ? in_slots<true>() : in_slots<false>();
+size_t stream_head_bytes(int K, int U, bool obs, int ring) {
+  const int R = ring ? ring : obs ? in_slots<true>() : in_slots<false>();
   const int R2 = obs ? out_slots<true>() : out_slots<false>();
   const size_t slot = ((size_t)U * 16 + (obs ? (size_t)U * 8 : 0) + 15) & ~(size_t)15;
   return kCtlBytes + (size_t)64 * K * sizeof(xf) + (size_t)64 * 16 * K + 2 * (size_t)R * slot +
@@ -950,6 +993,7 @@ int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
       case 4: return launch_stream_k<2, false, 2, 2>(a, st);
       case 5: return launch_stream_k<2, false, 2, 3>(a, st);
       case 6: return launch_stream_k<2, false, 3, 3>(a, st);
+      case 7: return launch_stream_k<2, false, 3, 4, 16>(a, st);
       default: break;
     }
   }

@@ -44,7 +44,7 @@ int set_fwd_bwd_variant(int v);
 // streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t stream);
 void set_stream_mix(int m);  // tuning only
-size_t stream_head_bytes(int K, int U, bool obs);  // LDS bytes besides the lattice rows
+size_t stream_head_bytes(int K, int U, bool obs, int ring = 0);  // LDS bytes besides the lattice rows
 int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only (tools/diag_fwd_bwd.py)
 
 // ---- beam-search decode (decode.hip) ----
