@@ -709,12 +709,17 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // Unrolled blocks of R steps aligned to R (slot offsets are compile-time); blocks that lie
   // inside one phase run without per-step guards. Factors for row r+PF are read into row r's
   // register buffer as soon as row r is done, so PF-1 steps hide the LDS latency (PF = 4 was
-  // tried: no faster before the cut, slower after it -- less ring slack). All LDS
+  // tried: no faster before the cut, slower after it -- less ring slack; so was issuing the
+  // read of row r+3 into a dead buffer before the step's arithmetic, which does keep three reads
+  // in flight in the .s: before the cut a step still costs ~300 cycles, so the LDS latency is
+  // not what bounds it; nor do the converter polls -- with them skipped (timing experiment) a
+  // step before the cut also takes ~300 cycles). All LDS
   // addresses are per-lane pointers prepared before the loop (lanes past U: junk / clamped).
   __builtin_amdgcn_s_setprio(3);
   const int d = role.d;
   int ready = 0;  // stream rows known converted
   auto wait_row = [&](int r) {  // r: a row that exists
+    if (EXP(3)) return;  // experiment (timing only, wrong results): chains never poll converters
     if (r >= ready)
       ready = spin_until<false>([&] { return first_missing<kNC>(ctl->conv[d], 0); }, r + 1, a.status, dg);
   };
