@@ -2,18 +2,21 @@
 //
 // Same lattice and the same split-exponent arithmetic as the two-wave kernel in fwd_bwd.hip
 // (DESIGN.md "Lattice semantics", "Split-exponent arithmetic"); bit-exact with
-// oracle/ssnt_oracle.c. What differs is who does what. One workgroup = one utterance, ten waves:
+// oracle/ssnt_oracle.c. What differs is who does what. One workgroup = one utterance; roles
+// (role_of) for the default K <= 2 mix, 16 waves:
 //
-//   wave 0      alpha chain: alpha[1..S-1], nothing else on its instruction stream
-//   wave 1      beta chain:  beta[S-1..0]
-//   waves 2..5  converters (2 per direction): load log_trans / log_obs rows from HBM, exp() them
+//   1 wave      alpha chain: alpha[1..S-1], nothing else on its instruction stream
+//   1 wave      beta chain:  beta[S-1..0]
+//   3 + 3 waves converters (per direction): load log_trans / log_obs rows from HBM, exp() them
 //               into split-exponent factors, write them to an R-slot LDS ring per direction.
 //               The forward ring holds the shift factors pre-shifted by one position
 //               (L[p] = Sh[p-1]), so the alpha chain's only cross-lane move is a DPP of its own
 //               row that the compiler folds into the multiply (v_mul_f32_dpp / v_add_u32_dpp).
-//   waves 6..9  gradient waves (2 per direction): one of them forms Z at the cut M = (S-1)>>1,
+//   4 + 4 waves gradient waves (per direction): one of them forms Z at the cut M = (S-1)>>1,
 //               then they emit d loss / d log_trans (and d loss / d log_obs) row by row behind
-//               the chains, reading the chain rows, the stored rows and the converted factors.
+//               the chains, reading the chain rows, the stored rows and the converters' ring
+//               (each cell is converted once per direction; these waves load nothing from HBM).
+// K >= 4 runs 2 + 2 + 2 per direction (10 waves: 168 VGPRs per wave, no spills).
 //
 // The cost model that shapes this (measured, tools/micro/): a lone wave issues one VALU
 // instruction per ~4.4 cycles whether or not the instructions depend on each other, so a chain
