@@ -269,12 +269,12 @@ __global__ __launch_bounds__(64) void k_lattice_decode(LatticeDecodeArgs a) {
     ff[w] = false;
   }
   float pre[kRowAhead][kRowRegs];
-  auto load_row = [&](int s, float* dst) {  // plain loads: the row does not depend on state
+  // unconditional (clamped) loads: a conditional load becomes a branch whose join waits
+  // vmcnt(0), i.e. for the load just issued -- which would undo the prefetch
+  auto load_row = [&](int s, float* dst) {  // the row does not depend on the beam state
 #pragma unroll
-    for (int q = 0; q < kRowRegs; ++q) {
-      const int idx = lane + 64 * q;
-      dst[q] = (s < T && idx < row_len) ? lat[(size_t)s * row_len + idx] : 0.0f;
-    }
+    for (int q = 0; q < kRowRegs; ++q)
+      dst[q] = lat[(size_t)min(s, T - 1) * row_len + min(lane + 64 * q, row_len - 1)];
   };
   if constexpr (STAGED) {
 #pragma unroll
@@ -355,13 +355,22 @@ __device__ __forceinline__ int wave_shr1(int v) {  // lane l gets lane l-1's v (
   return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
 }
 
+// Per-step outputs are staged in LDS and written out every kOutChunk steps: a global store
+// inside the step makes the next row prefetch's vmcnt wait also wait for that store (~1 us).
+constexpr int kOutChunk = 32;
 template <bool STAGED>
 __global__ __launch_bounds__(64) void k_lattice_decode_reg(LatticeDecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* rowbuf = reinterpret_cast<float*>(smem);  // (U,2): lattice row s (STAGED)
   const int b = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int W = a.W, T = a.T, U = a.U;
+  int* o_pred = reinterpret_cast<int*>(smem);       // (kOutChunk, W) each
+  float* o_lpb = reinterpret_cast<float*>(o_pred + kOutChunk * W);
+  int* o_nt = reinterpret_cast<int*>(o_lpb + kOutChunk * W);
+  int* o_nu = o_nt + kOutChunk * W;
+  int* o_br = o_nu + kOutChunk * W;
+  int* o_fin = o_br + kOutChunk * W;
+  float* rowbuf = reinterpret_cast<float*>(o_fin + kOutChunk * W);  // (U,2): lattice row s
   const int n = 2 * W;
   const u64 I = as_usize(a.input_length[b]);
   const float* lat = a.lattice + (size_t)b * T * U * 2;
@@ -370,12 +379,12 @@ __global__ __launch_bounds__(64) void k_lattice_decode_reg(LatticeDecodeArgs a) 
   float hist = 0.0f;
   int bt = 0, bu = 0, bfin = 0;
   float pre[kRowAhead][kRowRegs];
-  auto load_row = [&](int s, float* dst) {
+  // unconditional (clamped) loads: a conditional load becomes a branch whose join waits
+  // vmcnt(0), i.e. for the load just issued -- which would undo the prefetch
+  auto load_row = [&](int s, float* dst) {  // the row does not depend on the beam state
 #pragma unroll
-    for (int q = 0; q < kRowRegs; ++q) {
-      const int idx = lane + 64 * q;
-      dst[q] = (s < T && idx < row_len) ? lat[(size_t)s * row_len + idx] : 0.0f;
-    }
+    for (int q = 0; q < kRowRegs; ++q)
+      dst[q] = lat[(size_t)min(s, T - 1) * row_len + min(lane + 64 * q, row_len - 1)];
   };
   if constexpr (STAGED) {
 #pragma unroll
@@ -455,19 +464,33 @@ __global__ __launch_bounds__(64) void k_lattice_decode_reg(LatticeDecodeArgs a) 
     // ---- cyclic pad to W slots (src/lib.rs:163-168): slot i <- kept[i % nkept]
     const int src = (lane < W ? lane : 0) % (nkept > 0 ? nkept : 1);
     const float o_lp = __builtin_bit_cast(float, bperm_i(src, k_lp));
-    const int o_nt = bperm_i(src, k_nt), o_nu = bperm_i(src, k_nu), o_pk = bperm_i(src, k_pk);
+    const int o_nt_r = bperm_i(src, k_nt), o_nu_r = bperm_i(src, k_nu), o_pk = bperm_i(src, k_pk);
+    const int cs = s % kOutChunk;
     if (lane < W) {
-      const size_t o = ((size_t)b * T + s) * W + lane;
-      a.prediction[o] = o_pk & 1;
-      a.log_prob[o] = o_lp;
-      a.next_t[o] = o_nt;
-      a.next_u[o] = o_nu;
-      a.beam_branch[o] = o_pk >> 2;
-      a.next_fin[o] = ((o_pk >> 1) & 1) != 0;
+      const int o = cs * W + lane;
+      o_pred[o] = o_pk & 1;
+      o_lpb[o] = o_lp;
+      o_nt[o] = o_nt_r;
+      o_nu[o] = o_nu_r;
+      o_br[o] = o_pk >> 2;
+      o_fin[o] = (o_pk >> 1) & 1;
       hist = o_lp;
-      bt = o_nt;
-      bu = o_nu;
+      bt = o_nt_r;
+      bu = o_nu_r;
       bfin = (o_pk >> 1) & 1;
+    }
+    if (cs == kOutChunk - 1 || s == T - 1) {  // flush the chunk, coalesced (one wave: in order)
+      const int s_first = s - cs;
+      const int cnt = (cs + 1) * W;
+      const size_t g0 = ((size_t)b * T + s_first) * W;
+      for (int k = lane; k < cnt; k += 64) {
+        a.prediction[g0 + k] = o_pred[k];
+        a.log_prob[g0 + k] = o_lpb[k];
+        a.next_t[g0 + k] = o_nt[k];
+        a.next_u[g0 + k] = o_nu[k];
+        a.beam_branch[g0 + k] = o_br[k];
+        a.next_fin[g0 + k] = o_fin[k] != 0;
+      }
     }
     if constexpr (STAGED) __builtin_amdgcn_s_barrier();  // rowbuf is rewritten next step
   };
@@ -650,7 +673,8 @@ int launch_lattice_decode(const LatticeDecodeArgs& a, hipStream_t st) {
   const size_t lds = n * sizeof(Cand) + 2 * n * sizeof(int) + (size_t)a.W * (2 + 1 + 1 + 1) * 4 + a.W + 16 +
                      (staged ? (size_t)a.U * 2 * sizeof(float) : 0);
   if (2 * a.W <= 64) {  // one candidate per lane: the register-resident step
-    const size_t lds_reg = staged ? (size_t)a.U * 2 * sizeof(float) : 16;
+    const size_t lds_reg = (size_t)kOutChunk * a.W * 6 * sizeof(int) +
+                           (staged ? (size_t)a.U * 2 * sizeof(float) : 16);
     if (staged) hipLaunchKernelGGL(k_lattice_decode_reg<true>, dim3(a.B), dim3(64), lds_reg, st, a);
     else hipLaunchKernelGGL(k_lattice_decode_reg<false>, dim3(a.B), dim3(64), lds_reg, st, a);
   } else if (staged) {
