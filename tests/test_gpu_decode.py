@@ -228,3 +228,23 @@ print("unreachable")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "unreachable" not in r.stdout
     assert "could not find a duration sequence" in r.stderr
+
+
+@pytest.mark.parametrize("shape", [
+    (6, 37, 20, 1),    # W = 1, T not a multiple of the 4-row prefetch ring
+    (5, 70, 130, 4),   # U > 128: rows read from HBM directly; T spans three 32-step flushes
+    (4, 40, 30, 32),   # 2W = 64 candidates: every lane holds one
+    (3, 25, 16, 40),   # W > 32: the LDS step_wave kernel
+])
+@pytest.mark.parametrize("tie_rich", [False, True])
+def test_lattice_decode_paths(gpu, oracle, shape, tie_rich):
+    # every fused-decode path (register step staged / direct, LDS step) bit-exact vs the oracle
+    B, T, U, W = shape
+    lat = (oracle.synth_tie_rich_log_trans(B, T, U, seed=T) if tie_rich
+           else oracle.synth_log_trans(B, T, U, seed=T))
+    il = np.random.default_rng(U).integers(1, U + 1, size=B).astype(np.int32)
+    il[0] = U
+    want = oracle.v1_lattice_decode(lat, il, W)
+    got = gpu.lattice_beam_search_decode(_t(lat), _t(il), W)
+    for k, v in want.items():
+        assert np.array_equal(got[k].cpu().numpy(), v), k
