@@ -718,7 +718,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // not what bounds it; nor do the converter polls -- with them skipped (timing experiment) a
   // step before the cut also takes ~300 cycles). All LDS
   // addresses are per-lane pointers prepared before the loop (lanes past U: junk / clamped).
-  __builtin_amdgcn_s_setprio(3);
+  if (!EXP(9)) __builtin_amdgcn_s_setprio(3);  // experiment 9: chains at default priority
   const int d = role.d;
   int ready = 0;  // stream rows known converted
   auto wait_row = [&](int r) {  // r: a row that exists
