@@ -297,7 +297,7 @@ template <int K, bool OBS, bool LDS, int kNC, int kNH, int kRingSel>
 __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream(FwdBwdArgs a) {
   constexpr int kWaves = 2 + 2 * kNC + 2 * kNH;
   constexpr int R = kRingSel ? kRingSel : in_slots<OBS>();
-  constexpr int kR2 = out_slots<OBS>();
+  constexpr int kR2 = out_slots<OBS>() < R ? out_slots<OBS>() : R;
   static_assert(R % kR2 == 0, "ring sizes");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
@@ -962,7 +962,8 @@ int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
   if (a.U <= 64) return launch_stream_k<1, OBS, 3, 4>(a, st);
   if (a.U <= 128) return launch_stream_k<2, OBS, 3, 4>(a, st);
   if (a.U <= 256) return launch_stream_k<4, OBS, 2, 2>(a, st);
-  if (a.U <= 512) return launch_stream_k<8, OBS, 2, 2>(a, st);
+  // K = 8 (U <= 512, configs[4]): the two-wave kernel. The streaming kernel needs 4-slot rings to
+  // fit LDS there and then ran 2.2x slower (5.7 vs 2.6 ms at B=64 T=2000 U=400).
   return SSNT_ERR_UNSUPPORTED;
 #endif
 }
@@ -983,7 +984,8 @@ int diag_read(void* host, size_t bytes) {
 
 size_t stream_head_bytes(int K, int U, bool obs, int ring) {
   const int R = ring ? ring : obs ? in_slots<true>() : in_slots<false>();
-  const int R2 = obs ? out_slots<true>() : out_slots<false>();
+  const int R2o = obs ? out_slots<true>() : out_slots<false>();
+  const int R2 = R2o < R ? R2o : R;
   const size_t slot = ((size_t)U * 16 + (obs ? (size_t)U * 8 : 0) + 15) & ~(size_t)15;
   return kCtlBytes + (size_t)64 * K * sizeof(xf) + (size_t)64 * 16 * K + 2 * (size_t)R * slot +
          2 * (size_t)R2 * U * sizeof(xf);
