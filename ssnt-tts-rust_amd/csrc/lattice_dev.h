@@ -407,7 +407,7 @@ __device__ __forceinline__ void finish_loss_sum(const FwdBwdArgs& a, unsigned ta
     for (int i = lane; i < a.B; i += 64)
       ok &= (unsigned)(__hip_atomic_load(sum_granule(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
     if (__all(ok)) break;
-    if (spins > (1 << 20)) {  // bounded: report and give up (the sum is then not written)
+    if (spins > (1 << 24)) {  // bounded (~4 s): report and give up (the sum is then not written)
       if (lane == 0 && a.status) atomicOr(a.status, kStatusTimeout);
       return;
     }

@@ -220,3 +220,19 @@ def test_fused_loss_sum(gpu, oracle, kernel_variant, B):
     assert rc == 0
     torch.cuda.synchronize()
     assert lsum.cpu().numpy()[0] == want
+
+
+def test_fused_loss_sum_more_workgroups_than_cus(gpu, oracle, kernel_variant):
+    # B = 2048 > 256 CUs: workgroup 0 waits for workgroups dispatched after it; the sum must still
+    # be formed (and the state re-armed for the next call)
+    dev = torch.device("cuda:0")
+    B, T, U = 2048, 24, 16
+    lt = oracle.synth_log_trans(B, T, U, seed=5)
+    x = torch.from_numpy(lt).to(dev)
+    sl = torch.full((B,), T, dtype=torch.int32, device=dev)
+    pl = torch.full((B,), U, dtype=torch.int32, device=dev)
+    o = oracle.fwd_bwd_xf(lt, [T] * B, [U] * B)
+    for _ in range(2):
+        r = gpu.ssnt_fwd_bwd(x, sl, pl, loss_sum=True, check=True)
+        assert np.array_equal(r["loss"].cpu().numpy(), o["loss"])
+        assert r["loss_sum"].cpu().numpy()[0] == _wave_order_sum(o["loss"])
