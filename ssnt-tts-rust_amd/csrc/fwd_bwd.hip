@@ -340,8 +340,8 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
 }
 
 int set_fwd_bwd_variant(int v) {
-  // 0 stream, 1 two-wave; 2..8: stream with another wave mix / ring size (tuning only)
-  if (v < 0 || v > 8) return SSNT_ERR_INVALID_ARG;
+  // 0 stream, 1 two-wave; 2..10: stream with another wave mix / ring / publication (tuning only)
+  if (v < 0 || v > 10) return SSNT_ERR_INVALID_ARG;
   g_variant = v >= 2 ? 0 : v;
   set_stream_mix(v >= 2 ? v - 1 : 0);
   return SSNT_OK;

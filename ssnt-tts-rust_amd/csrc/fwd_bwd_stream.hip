@@ -296,7 +296,9 @@ __device__ __forceinline__ void lds_xrow_st(xf* p, const XRow<K>& r) {
 template <int K, bool OBS, bool LDS, int kNC, int kNH, int kRingSel>
 __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream(FwdBwdArgs a) {
   constexpr int kWaves = 2 + 2 * kNC + 2 * kNH;
-  constexpr int R = kRingSel ? kRingSel : in_slots<OBS>();
+  // kRingSel: ring slots (0 = default); tuning variants: +100 publish every step past the cut,
+  // +200 every 2 steps before it
+  constexpr int R = (kRingSel % 100) ? (kRingSel % 100) : in_slots<OBS>();
   constexpr int kR2 = out_slots<OBS>() < R ? out_slots<OBS>() : R;
   static_assert(R % kR2 == 0, "ring sizes");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -765,8 +767,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // Phase 2 (past the cut) publishes every H2 steps instead: there the gradient waves read each
   // factor slot right behind the chain and the converters need it back, so the hand-off
   // chain -> gradient waves -> converters -> chain has to close within the ring's slack.
-  using H1 = std::integral_constant<int, (R >= 16 ? R / 4 : R / 2)>;
-  using H2 = std::integral_constant<int, (R >= 16 ? R / 8 : (R / 4 > 2 ? R / 4 : 2))>;
+  using H1 = std::integral_constant<int, (kRingSel >= 200 ? 2 : R >= 16 ? R / 4 : R / 2)>;
+  using H2 = std::integral_constant<int, ((kRingSel >= 100 && kRingSel < 200) ? 1 : R >= 16 ? R / 8 : (R / 4 > 2 ? R / 4 : 2))>;
   auto run = [&](auto Hc, int lo, int hi, auto&& step, auto&& hwait) {
     constexpr int HS = decltype(Hc)::value;
     static_assert(R % HS == 0, "sub-blocks tile the ring");
@@ -983,6 +985,7 @@ int diag_read(void* host, size_t bytes) {
 }
 
 size_t stream_head_bytes(int K, int U, bool obs, int ring) {
+  ring %= 100;
   const int R = ring ? ring : obs ? in_slots<true>() : in_slots<false>();
   const int R2o = obs ? out_slots<true>() : out_slots<false>();
   const int R2 = R2o < R ? R2o : R;
@@ -1004,6 +1007,8 @@ int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
       case 5: return launch_stream_k<2, false, 2, 3>(a, st);
       case 6: return launch_stream_k<2, false, 3, 3>(a, st);
       case 7: return launch_stream_k<2, false, 3, 4, 16>(a, st);
+      case 8: return launch_stream_k<2, false, 3, 4, 108>(a, st);
+      case 9: return launch_stream_k<2, false, 3, 4, 208>(a, st);
       default: break;
     }
   }

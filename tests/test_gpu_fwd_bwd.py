@@ -152,9 +152,9 @@ def test_autograd_function(gpu, oracle):
     assert np.array_equal(x.grad.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_tuning_wave_mixes_bit_exact(gpu, oracle, kernel_variant, variant):
-    # the converter / gradient wave mixes of the streaming kernel (ssnt_fwd_bwd_set_variant 2..7,
+    # the converter / gradient wave mixes, ring sizes and publication periods of the streaming kernel (variants 2..10,
     # K = 2 shapes) must be bit-identical to the oracle like the default mix
     if kernel_variant != 0:
         pytest.skip("mix variants are streaming-kernel variants")
