@@ -107,5 +107,8 @@ int main() {
   RUN(8, 0, "slot reads + row store + lane-0 counter store every 2nd step")
   RUN(10, 0, "reads 2 rows ahead + row store + counter store")
   RUN(10, 9, "reads 2 ahead + row store + ctr + 9 waves spinning")
+  RUN(10, 15, "reads 2 ahead + row store + ctr + 15 waves spinning")
+  RUN(5, 15, "+ 15 co-resident waves dense VALU")
+  RUN(6, 15, "+ 15 co-resident waves LDS read/write")
   return 0;
 }
