@@ -48,17 +48,44 @@ def synth(B, T, U, seed, dev):
     return torch.log_softmax(z, dim=-1).contiguous()
 
 
+def host_cpu_info():
+    """The cores this process may run on: sched affinity, capped by a cgroup CPU quota when one
+    is set (cpu.max); plus nproc and the CPU model string, so the baseline states its host."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    model = "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"usable": usable, "affinity": aff, "nproc": os.cpu_count(), "cgroup_quota": quota,
+            "model": model}
+
+
 def cpu_baseline(B, T, U):
-    """Time the C oracle on this host: repeated config-2 batches for ~2 s of wall time."""
+    """Time the C oracle on this host over every usable core (OpenMP over the batch, like the
+    reference's rayon par_chunks): repeated full config-2 batches for ~10 s of wall time, plus
+    a one-thread figure on a 16-utterance sample."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    info = host_cpu_info()
+    threads = info["usable"]
     lt = O.synth_log_trans(B, T, U, seed=0)
     sl, pl = [T] * B, [U] * B
-    O.fwd_bwd_xf(lt[:8], sl[:8], pl[:8], n_threads=threads)  # warm-up
+    O.fwd_bwd_xf(lt, sl, pl, n_threads=threads)  # warm-up (first touch of every page)
     times = []
-    t_end = time.perf_counter() + 2.0
-    while len(times) < 3 or time.perf_counter() < t_end:
+    t_end = time.perf_counter() + 10.0
+    while len(times) < 5 or time.perf_counter() < t_end:
         t0 = time.perf_counter()
         O.fwd_bwd_xf(lt, sl, pl, n_threads=threads)
         times.append(time.perf_counter() - t0)
@@ -68,9 +95,9 @@ def cpu_baseline(B, T, U):
     single = 16 * T * U / (time.perf_counter() - t0)
     return {"value": B * T * U / med, "unit": "cells/s", "cores": threads, "kind": "port",
             "sample": f"{len(times)} x full B={B} T={T} U={U} fwd-bwd+grad batches "
-                      f"(median {med * 1e3:.1f} ms/batch, {threads} OpenMP threads); "
-                      f"1 thread: {single:.3e} cells/s",
-            "single_thread_value": single}
+                      f"(median {med * 1e3:.1f} ms/batch, {threads} OpenMP threads = every "
+                      f"usable core); 1 thread: {single:.3e} cells/s",
+            "single_thread_value": single, "host": info}
 
 
 def pmc_traffic():

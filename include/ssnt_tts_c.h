@@ -191,6 +191,36 @@ int ssnt_lattice_beam_search_decode_device(const float *lattice, const int *inpu
                                            int *beam_branch, int *best_beam_branch,
                                            int *best_t_history, int *status, void *stream);
 
+/* Fused multi-step v2 duration-class decode (BASELINE configs[4] "v2 path"). Every beam starts
+ * at t = u = 0, log-prob 0, total_duration 0, not finished; step s runs the exact
+ * ssnt_tts_v2_beam_search_decode step (src/v2.rs:221-339, max_beam_width = beam_width) on
+ * h = logits[b, s] (W,D) and feeds its outputs back as the next state -- what the TF decode loop
+ * does around the per-step op, one launch instead of max_steps. logits (B,T,W,D); per-step
+ * outputs (B,T,W). Then, in the same launch, every final slot w is backtraced
+ * (src/v2_util.rs:6-36 with final_branch = [0..W)): ordered_beam_branch (B,W,T), the class
+ * chosen at each step of each path (path_prediction, B,W,T) and the duration it added
+ * (duration, B,W,T; sums to the path's final total, the input of
+ * ssnt_upsample_source_indexes). The three path outputs may be NULL. An utterance where no
+ * candidate survives (the reference panics, src/v2.rs:292) sets SSNT_ERR_NO_CANDIDATE in
+ * `status` and its outputs are unspecified. New: the reference steps once per call. */
+int ssnt_v2_lattice_beam_search_decode_device(
+    const float *logits, const int *duration_table, const int *input_length,
+    const int *output_length, int batch_size, int max_steps, int beam_width,
+    int duration_class_size, int zero_duration_id, bool allow_skip, bool test_mode,
+    int *prediction, float *log_probs, int *next_t, int *next_u, bool *next_is_finished,
+    int *next_total_duration, int *beam_branch, int *ordered_beam_branch, int *path_prediction,
+    int *duration, int *status, void *stream);
+
+/* Fused multi-step tone-latent decode (BASELINE configs[4] "tone_latent path"): as
+ * ssnt_v2_lattice_beam_search_decode_device with the tone step (src/tone_latent.rs:144-234),
+ * logits (B,T,W,C); path outputs ordered_beam_branch and path_prediction (the tone sequence of
+ * each final slot, the input of the edit-distance evaluation) may be NULL. */
+int ssnt_tone_latent_lattice_beam_search_decode_device(
+    const float *logits, const int *input_length, int batch_size, int max_steps, int beam_width,
+    int tone_class_size, int empty_tone_id, int *prediction, float *log_probs, int *next_t,
+    int *next_u, bool *next_is_finished, int *beam_branch, int *ordered_beam_branch,
+    int *path_prediction, int *status, void *stream);
+
 /* Batched backtraces / utilities, device pointers. */
 int ssnt_extract_best_beam_branch_device(const int *best_final_branch, const int *beam_branch,
                                          const int *t_history, int batch_size, int beam_width,

@@ -180,6 +180,57 @@ def v1_lattice_decode(lattice, input_length, beam_width, n_threads=0):
     return o
 
 
+def _fused_outs(B, T, W, v2):
+    o = dict(prediction=np.zeros((B, T, W), np.int32), log_prob=np.zeros((B, T, W), np.float32),
+             next_t=np.zeros((B, T, W), np.int32), next_u=np.zeros((B, T, W), np.int32),
+             next_is_finished=np.zeros((B, T, W), np.bool_))
+    if v2:
+        o["next_total_duration"] = np.zeros((B, T, W), np.int32)
+    o["beam_branch"] = np.zeros((B, T, W), np.int32)
+    o["ordered_beam_branch"] = np.zeros((B, W, T), np.int32)
+    o["path_prediction"] = np.zeros((B, W, T), np.int32)
+    if v2:
+        o["duration"] = np.zeros((B, W, T), np.int32)
+    return o
+
+
+def v2_lattice_decode(logits, duration_table, input_length, output_length, zero_duration_id,
+                      allow_skip, test_mode, n_threads=0):
+    """Fused multi-step v2 decode over per-step logits (B,T,W,D) (configs[4] v2 path): the
+    v2 step (src/v2.rs:221-339) T times from the all-zero state, then the backtrace of every
+    final slot (src/v2_util.rs:6-36). Returns (outs, status); test_mode zeroes output_length
+    like the reference wrapper (__init__.py:47)."""
+    lg = _f32(logits)
+    B, T, W, D = lg.shape
+    ol = np.zeros(B, np.int32) if test_mode else _i32(output_length)
+    o = _fused_outs(B, T, W, True)
+    rc = lib().oracle_v2_lattice_decode(
+        B, T, W, D, _p(lg, _f32p), _p(_i32(duration_table), _i32p), _p(_i32(input_length), _i32p),
+        _p(ol, _i32p), int(zero_duration_id), ctypes.c_bool(allow_skip), ctypes.c_bool(test_mode),
+        _p(o["prediction"], _i32p), _p(o["log_prob"], _f32p), _p(o["next_t"], _i32p),
+        _p(o["next_u"], _i32p), _p(o["next_is_finished"], _boolp),
+        _p(o["next_total_duration"], _i32p), _p(o["beam_branch"], _i32p),
+        _p(o["ordered_beam_branch"], _i32p), _p(o["path_prediction"], _i32p),
+        _p(o["duration"], _i32p), int(n_threads))
+    return o, rc
+
+
+def tone_lattice_decode(logits, input_length, empty_tone_id, n_threads=0):
+    """Fused multi-step tone-latent decode over per-step logits (B,T,W,C) (configs[4] tone
+    path): the tone step (src/tone_latent.rs:144-234) T times, then every final slot's path."""
+    lg = _f32(logits)
+    B, T, W, C = lg.shape
+    o = _fused_outs(B, T, W, False)
+    rc = lib().oracle_tone_lattice_decode(
+        B, T, W, C, _p(lg, _f32p), _p(_i32(input_length), _i32p), int(empty_tone_id),
+        _p(o["prediction"], _i32p), _p(o["log_prob"], _f32p), _p(o["next_t"], _i32p),
+        _p(o["next_u"], _i32p), _p(o["next_is_finished"], _boolp), _p(o["beam_branch"], _i32p),
+        _p(o["ordered_beam_branch"], _i32p), _p(o["path_prediction"], _i32p), int(n_threads))
+    if rc != 0:
+        raise RuntimeError(f"oracle_tone_lattice_decode status {rc}")
+    return o
+
+
 def fwd_bwd_xf(log_trans, step_len, pos_len, log_obs=None, flags=FLAG_TERMINAL_EMIT,
                debug=False, n_threads=0):
     """Exact split-exponent f32 fwd-bwd (the arithmetic the HIP kernel reproduces bit-exactly)."""
@@ -245,3 +296,54 @@ def synth_tie_rich_log_trans(B, T, U, seed=0):
     pe = p
     ps = (np.float32(1.0) - p).astype(np.float32)
     return np.log(np.concatenate([pe, ps], axis=-1).astype(np.float32)).astype(np.float32)
+
+
+def synth_durations(B, I, O, D, seed=0):
+    """Per-utterance duration sequences d (B,I) in [1, D-1] with sum == O[b] over the first
+    I[b] positions (0 after), each prefix inside v2's band around the diagonal
+    (src/v2.rs:94-104): the path the v2 decode must find."""
+    rng = np.random.default_rng(seed)
+    I = np.broadcast_to(np.asarray(I, np.int64), (B,))
+    O = np.broadcast_to(np.asarray(O, np.int64), (B,))
+    d = np.zeros((B, int(I.max())), np.int32)
+    for b in range(B):
+        n, tot = int(I[b]), int(O[b])
+        base = tot / n
+        x = np.clip(np.round(base + rng.normal(0, 1.0, n)), 1, D - 1).astype(np.int64)
+        # fix the sum one step at a time, on random positions with room
+        while x.sum() != tot:
+            j = rng.integers(n)
+            if x.sum() < tot and x[j] < D - 1:
+                x[j] += 1
+            elif x.sum() > tot and x[j] > 1:
+                x[j] -= 1
+        d[b, :n] = x
+    return d
+
+
+def synth_v2_logits(durations, W, D, seed=0, margin=8.0, tie_rich=False):
+    """Per-step logits (B,T,W,D) peaked at the sampled duration class of each step (class index
+    == duration with duration_table = [0..D-1]). tie_rich: ln of probabilities in {0.1..0.3}
+    with 0.9 at the peak (f32), so equal log-probs are everywhere."""
+    rng = np.random.default_rng(seed)
+    B, T = durations.shape
+    if tie_rich:
+        p = rng.integers(1, 4, size=(B, T, W, D)).astype(np.float32) / np.float32(10.0)
+        onehot = np.eye(D, dtype=bool)[durations][:, :, None, :]
+        p = np.where(onehot, np.float32(0.9), p).astype(np.float32)
+        return np.log(p).astype(np.float32)
+    z = rng.standard_normal((B, T, W, D)).astype(np.float32)
+    z += np.float32(margin) * np.eye(D, dtype=np.float32)[durations][:, :, None, :]
+    m = z.max(axis=-1, keepdims=True)
+    return (z - (m + np.log(np.exp(z - m).sum(axis=-1, keepdims=True)))).astype(np.float32)
+
+
+def synth_tone_logits(B, T, W, C, seed=0, tie_rich=False):
+    """Per-step tone logits (B,T,W,C): log_softmax of N(0,1.5^2), or tie-rich ln(p) with p in
+    {0.1..0.9}."""
+    rng = np.random.default_rng(seed)
+    if tie_rich:
+        return np.log((rng.integers(1, 10, size=(B, T, W, C)) / 10.0).astype(np.float32)).astype(np.float32)
+    z = rng.standard_normal((B, T, W, C)).astype(np.float32) * np.float32(1.5)
+    m = z.max(axis=-1, keepdims=True)
+    return (z - (m + np.log(np.exp(z - m).sum(axis=-1, keepdims=True)))).astype(np.float32)

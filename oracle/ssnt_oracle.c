@@ -45,7 +45,7 @@
 #define ORC_ERR_INVALID 1
 
 /* ------------------------------------------------------------------------------------------
- * Decode: candidate record (src/lib.rs:70-88, src/v2.rs:169-189, src/tone_latent.rs:437-455).
+ * Decode: candidate record (src/lib.rs:70-88, src/v2.rs:169-189, src/tone_latent.rs:98-101,208-234).
  * next_t / next_u are Rust `usize`: the i32 inputs are converted with `as usize` (sign
  * extension, src/lib.rs:135-136) and written back `as i32` (src/lib.rs:141-142).
  * ---------------------------------------------------------------------------------------- */
@@ -233,6 +233,30 @@ static int v2_internal(const v2_ctx *c, const float *h, const float *hist, const
     return n;
 }
 
+/* One batch element of the v2 step: beam_search_kernel (src/v2.rs:269-309) over the W beams.
+ * buf holds W*D + W candidates, res Wmax. Returns 0, or ORC_ERR_NO_CANDIDATE where the reference
+ * panics (assert_ne!(n_results, 0), src/v2.rs:292). */
+static int v2_step_one(const v2_ctx *c, int W, int Wmax, const float *hb, const float *hist,
+                       const bool *fin, const int32_t *t, const int32_t *u, cand_t *buf,
+                       cand_t *res) {
+    int n = 0;
+    for (int w = 0; w < W; ++w)
+        n += v2_internal(c, hb, hist, fin, w, as_usize(t[w]), as_usize(u[w]), buf + n);
+    sort_desc_stable(buf, n);
+    n = dedup(buf, n, true);
+    int diag = -1; /* src/v2.rs:283-289: first sorted+deduped candidate on the diagonal */
+    if (!c->test_mode)
+        for (int i = 0; i < n; ++i)
+            if (v2_on_diagonal(c, &buf[i])) {
+                diag = i;
+                break;
+            }
+    if (n == 0) return ORC_ERR_NO_CANDIDATE;
+    for (int i = 0; i < Wmax; ++i) res[i] = buf[i % n]; /* src/v2.rs:293-297 */
+    if (diag >= 0) res[Wmax - 1] = buf[diag];             /* src/v2.rs:298-303 */
+    return ORC_OK;
+}
+
 /* Batched v2 step: SsntTtsV2Cpu::beam_search_decode (src/v2.rs:221-309). */
 int oracle_v2_step(int B, int W, int Wmax, int D, const float *h, const float *hist,
                    const bool *fin, const int32_t *total, const int32_t *table, const int32_t *t,
@@ -247,36 +271,42 @@ int oracle_v2_step(int B, int W, int Wmax, int D, const float *h, const float *h
     for (int b = 0; b < B; ++b) {
         v2_ctx c = {as_usize(input_length[b]), as_usize(output_length[b]), total + (size_t)b * W,
                     table, D, zero_duration_id, allow_skip, test_mode};
-        const float *hb = h + (size_t)b * W * D;
-        int n = 0;
-        for (int w = 0; w < W; ++w)
-            n += v2_internal(&c, hb, hist + (size_t)b * W, fin + (size_t)b * W, w,
-                             as_usize(t[(size_t)b * W + w]), as_usize(u[(size_t)b * W + w]),
-                             buf + n);
-        sort_desc_stable(buf, n);
-        n = dedup(buf, n, true);
-        int diag = -1; /* src/v2.rs:283-289: first sorted+deduped candidate on the diagonal */
-        if (!test_mode)
-            for (int i = 0; i < n; ++i)
-                if (v2_on_diagonal(&c, &buf[i])) {
-                    diag = i;
-                    break;
-                }
-        if (n == 0) { /* assert_ne!(n_results, 0) -> panic, src/v2.rs:292 */
+        const size_t o = (size_t)b * W;
+        if (v2_step_one(&c, W, Wmax, h + o * D, hist + o, fin + o, t + o, u + o, buf, res) != ORC_OK) {
             status = ORC_ERR_NO_CANDIDATE;
             continue;
         }
-        for (int i = 0; i < Wmax; ++i) res[i] = buf[i % n]; /* src/v2.rs:293-297 */
-        if (diag >= 0) res[Wmax - 1] = buf[diag];             /* src/v2.rs:298-303 */
-        const size_t o = (size_t)b * Wmax;
-        write_results(res, Wmax, prediction + o, log_probs + o, next_t + o, next_u + o,
-                      next_fin + o, next_tot + o, beam_branch + o);
+        const size_t ow = (size_t)b * Wmax;
+        write_results(res, Wmax, prediction + ow, log_probs + ow, next_t + ow, next_u + ow,
+                      next_fin + ow, next_tot + ow, beam_branch + ow);
     }
     free(buf);
     return status;
 }
 
 /* ---------------------------- tone latent (src/tone_latent.rs:144-234) ------------------ */
+/* One batch element: beam_search_kernel (src/tone_latent.rs:184-206). */
+static void tone_step_one(uint64_t I, int W, int Wmax, int C, const float *hb, const float *hi,
+                          const bool *fb, const int32_t *t, const int32_t *u, int empty_tone_id,
+                          cand_t *buf, cand_t *res) {
+    int n = 0;
+    for (int w = 0; w < W; ++w) {
+        const uint64_t tw = as_usize(t[w]), uw = as_usize(u[w]);
+        /* decode_beam_at (src/tone_latent.rs:79-96): undefined past the input or finished ->
+         * one finished "padding" candidate (src/tone_latent.rs:212-219) */
+        if (!(tw < I) || fb[w]) {
+            buf[n++] = (cand_t){empty_tone_id, hi[w], tw, uw, true, w, 0};
+            continue;
+        }
+        /* every class, never finished (src/tone_latent.rs:87-93, 220-231) */
+        for (int i = 0; i < C; ++i)
+            buf[n++] = (cand_t){i, hi[w] + hb[w * C + i], tw + 1, uw + 1, false, w, 0};
+    }
+    sort_desc_stable(buf, n);
+    n = dedup(buf, n, false);
+    for (int i = 0; i < Wmax; ++i) res[i] = buf[i % n];
+}
+
 int oracle_tone_step(int B, int W, int Wmax, int C, const float *h, const float *hist,
                      const bool *fin, const int32_t *t, const int32_t *u,
                      const int32_t *input_length, int empty_tone_id, int32_t *prediction,
@@ -286,26 +316,12 @@ int oracle_tone_step(int B, int W, int Wmax, int C, const float *h, const float 
     cand_t *buf = (cand_t *)malloc(sizeof(cand_t) * ((size_t)W * C + W + Wmax));
     cand_t *res = buf + (size_t)W * C + W;
     for (int b = 0; b < B; ++b) {
-        const uint64_t I = as_usize(input_length[b]);
-        const float *hb = h + (size_t)b * W * C;
-        const float *hi = hist + (size_t)b * W;
-        const bool *fb = fin + (size_t)b * W;
-        int n = 0;
-        for (int w = 0; w < W; ++w) {
-            const uint64_t tw = as_usize(t[(size_t)b * W + w]), uw = as_usize(u[(size_t)b * W + w]);
-            if (!(tw < I) || fb[w]) { /* src/tone_latent.rs:418-424, 549-558 */
-                buf[n++] = (cand_t){empty_tone_id, hi[w], tw, uw, true, w, 0};
-                continue;
-            }
-            for (int i = 0; i < C; ++i) /* src/tone_latent.rs:426-433, 560-570 */
-                buf[n++] = (cand_t){i, hi[w] + hb[w * C + i], tw + 1, uw + 1, false, w, 0};
-        }
-        sort_desc_stable(buf, n);
-        n = dedup(buf, n, false);
-        for (int i = 0; i < Wmax; ++i) res[i] = buf[i % n];
-        const size_t o = (size_t)b * Wmax;
-        write_results(res, Wmax, prediction + o, log_probs + o, next_t + o, next_u + o,
-                      next_fin + o, NULL, beam_branch + o);
+        const size_t o = (size_t)b * W;
+        tone_step_one(as_usize(input_length[b]), W, Wmax, C, h + o * C, hist + o, fin + o, t + o,
+                      u + o, empty_tone_id, buf, res);
+        const size_t ow = (size_t)b * Wmax;
+        write_results(res, Wmax, prediction + ow, log_probs + ow, next_t + ow, next_u + ow,
+                      next_fin + ow, NULL, beam_branch + ow);
     }
     free(buf);
     return ORC_OK;
@@ -440,6 +456,134 @@ int oracle_v1_lattice_decode(int B, int T, int U, int W, const float *lattice,
     return ORC_OK;
 }
 
+/* Backtrace of every final slot w (v2_util::order_beam_branch, src/v2_util.rs:6-36, with
+ * final_branch = [0..W)) plus the per-path class sequence and, when tot is given, the duration
+ * each step added along the path (next_total_duration of the slot minus that of its parent;
+ * initial totals are 0). Outputs (W,T) rows of one batch element. */
+static void fused_paths(int T, int W, const int32_t *pred, const int32_t *branch,
+                        const int32_t *tot, int32_t *ordered, int32_t *path_pred,
+                        int32_t *duration) {
+    for (int w = 0; w < W; ++w) {
+        int32_t cur = w;
+        for (int s = T - 1; s >= 0; --s) {
+            const int32_t parent = branch[(size_t)s * W + cur];
+            if (ordered) ordered[(size_t)w * T + s] = cur;
+            if (path_pred) path_pred[(size_t)w * T + s] = pred[(size_t)s * W + cur];
+            if (duration)
+                duration[(size_t)w * T + s] =
+                    tot[(size_t)s * W + cur] - (s > 0 ? tot[(size_t)(s - 1) * W + parent] : 0);
+            cur = parent;
+        }
+    }
+}
+
+/* Fused multi-step v2 decode (BASELINE configs[4] "v2 path"): every beam starts at t=u=0,
+ * log-prob 0, total_duration 0, not finished; step s runs the exact v2 step
+ * (src/v2.rs:221-339, Wmax = W) with h = logits[b, s] (W,D) -- the per-step op's input, replayed
+ * from a precomputed (B,T,W,D) tensor -- and feeds its outputs back as the next state (the TF
+ * decode loop's role). Then fused_paths. An utterance that hits "no candidate" (the reference
+ * panics, src/v2.rs:292) stops there; the call returns ORC_ERR_NO_CANDIDATE and that
+ * utterance's remaining outputs are unspecified. */
+int oracle_v2_lattice_decode(int B, int T, int W, int D, const float *logits,
+                             const int32_t *table, const int32_t *input_length,
+                             const int32_t *output_length, int zero_duration_id, bool allow_skip,
+                             bool test_mode, int32_t *pred, float *lp, int32_t *next_t,
+                             int32_t *next_u, bool *fin, int32_t *tot, int32_t *branch,
+                             int32_t *ordered, int32_t *path_pred, int32_t *duration,
+                             int n_threads) {
+    if (W <= 0 || D <= 0 || T <= 0) return ORC_ERR_INVALID;
+    int status = ORC_OK;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic)
+#endif
+    for (int b = 0; b < B; ++b) {
+        float *hist = (float *)calloc(W, sizeof(float));
+        bool *f = (bool *)calloc(W, sizeof(bool));
+        int32_t *tt = (int32_t *)calloc(W, sizeof(int32_t));
+        int32_t *uu = (int32_t *)calloc(W, sizeof(int32_t));
+        int32_t *total = (int32_t *)calloc(W, sizeof(int32_t));
+        cand_t *buf = (cand_t *)malloc(sizeof(cand_t) * ((size_t)W * D + 2 * W));
+        const v2_ctx c0 = {as_usize(input_length[b]), as_usize(output_length[b]), NULL, table, D,
+                           zero_duration_id, allow_skip, test_mode};
+        bool ok = true;
+        for (int s = 0; s < T; ++s) {
+            v2_ctx c = c0;
+            c.total = total;
+            cand_t *res = buf + (size_t)W * D + W;
+            if (v2_step_one(&c, W, W, logits + ((size_t)b * T + s) * W * D, hist, f, tt, uu, buf,
+                            res) != ORC_OK) {
+                ok = false;
+                break;
+            }
+            const size_t o = ((size_t)b * T + s) * W;
+            write_results(res, W, pred + o, lp + o, next_t + o, next_u + o, fin + o, tot + o,
+                          branch + o);
+            for (int w = 0; w < W; ++w) {
+                hist[w] = lp[o + w];
+                f[w] = fin[o + w];
+                tt[w] = next_t[o + w];
+                uu[w] = next_u[o + w];
+                total[w] = tot[o + w];
+            }
+        }
+        if (ok) {
+            const size_t o = (size_t)b * T * W;
+            fused_paths(T, W, pred + o, branch + o, tot + o, ordered ? ordered + o : NULL,
+                        path_pred ? path_pred + o : NULL, duration ? duration + o : NULL);
+        } else {
+#ifdef _OPENMP
+#pragma omp atomic write
+#endif
+            status = ORC_ERR_NO_CANDIDATE;
+        }
+        free(hist); free(f); free(tt); free(uu); free(total); free(buf);
+    }
+    return status;
+}
+
+/* Fused multi-step tone-latent decode (BASELINE configs[4] "tone_latent path"): as
+ * oracle_v2_lattice_decode with the tone step (src/tone_latent.rs:144-234), h = logits[b, s]
+ * (W,C); then fused_paths (no durations). */
+int oracle_tone_lattice_decode(int B, int T, int W, int C, const float *logits,
+                               const int32_t *input_length, int empty_tone_id, int32_t *pred,
+                               float *lp, int32_t *next_t, int32_t *next_u, bool *fin,
+                               int32_t *branch, int32_t *ordered, int32_t *path_pred,
+                               int n_threads) {
+    if (W <= 0 || C <= 0 || T <= 0) return ORC_ERR_INVALID;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic)
+#endif
+    for (int b = 0; b < B; ++b) {
+        float *hist = (float *)calloc(W, sizeof(float));
+        bool *f = (bool *)calloc(W, sizeof(bool));
+        int32_t *tt = (int32_t *)calloc(W, sizeof(int32_t));
+        int32_t *uu = (int32_t *)calloc(W, sizeof(int32_t));
+        cand_t *buf = (cand_t *)malloc(sizeof(cand_t) * ((size_t)W * C + 2 * W));
+        const uint64_t I = as_usize(input_length[b]);
+        for (int s = 0; s < T; ++s) {
+            cand_t *res = buf + (size_t)W * C + W;
+            tone_step_one(I, W, W, C, logits + ((size_t)b * T + s) * W * C, hist, f, tt, uu,
+                          empty_tone_id, buf, res);
+            const size_t o = ((size_t)b * T + s) * W;
+            write_results(res, W, pred + o, lp + o, next_t + o, next_u + o, fin + o, NULL,
+                          branch + o);
+            for (int w = 0; w < W; ++w) {
+                hist[w] = lp[o + w];
+                f[w] = fin[o + w];
+                tt[w] = next_t[o + w];
+                uu[w] = next_u[o + w];
+            }
+        }
+        const size_t o = (size_t)b * T * W;
+        fused_paths(T, W, pred + o, branch + o, NULL, ordered ? ordered + o : NULL,
+                    path_pred ? path_pred + o : NULL, NULL);
+        free(hist); free(f); free(tt); free(uu); free(buf);
+    }
+    return ORC_OK;
+}
+
 /* ==========================================================================================
  * Forward-backward emit/shift lattice (DESIGN.md "Lattice semantics").
  *
@@ -466,7 +610,9 @@ static const float L2E = 0x1.715476p+0f;
 static const float LN2HI = 0x1.62e400p-1f;  /* 0x3f317200 */
 static const float LN2LO = 0x1.7f7d1cp-20f; /* 0x35bfbe8e */
 static const float SQRTH = 0x1.6a09e6p-1f;
-/* e^r on [-ln2/2, ln2/2], deg 6 (fit: tools/fit_poly.py) */
+/* e^r on [-ln2/2, ln2/2], deg 6. The coefficients are fixed constants of the arithmetic
+ * definition (shared with csrc/xf_math.h); their accuracy against float64 exp/log is checked by
+ * tests/test_oracle_fwd_bwd.py (the fit script was not kept). */
 static const float EC[7] = {0x1p+0f, 0x1p+0f, 0x1p-1f, 0x1.555404p-3f, 0x1.555464p-5f,
                             0x1.126facp-7f, 0x1.6da758p-10f};
 /* ln(1+t)/t on [sqrt(.5)-1, sqrt(2)-1], deg 8 */

@@ -613,6 +613,23 @@ int ssnt_lattice_beam_search_decode_device(const float* lattice, const int* inpu
   if (!lattice || !input_length || !prediction || !log_probs || !next_t || !next_u ||
       !next_is_finished || !beam_branch || !best_beam_branch || !best_t_history)
     return SSNT_ERR_INVALID_ARG;
+  FusedDecodeArgs a{};
+  a.variant = Variant::V1;
+  a.B = batch_size; a.T = max_steps; a.U = max_pos; a.W = beam_width; a.C = 2;
+  a.src = lattice; a.input_length = input_length;
+  a.prediction = prediction; a.log_prob = log_probs; a.next_t = next_t; a.next_u = next_u;
+  a.next_fin = next_is_finished; a.beam_branch = beam_branch;
+  a.best_beam_branch = best_beam_branch; a.best_t_history = best_t_history; a.status = status;
+  return launch_fused_decode(a, as_stream(stream));
+}
+
+// round-2 A/B only (not in the public header): the round-1 fused v1 kernel + k_backtrace
+int ssnt_lattice_decode_r1_device(const float* lattice, const int* input_length, int batch_size,
+                                  int max_steps, int max_pos, int beam_width, int* prediction,
+                                  float* log_probs, int* next_t, int* next_u,
+                                  bool* next_is_finished, int* beam_branch,
+                                  int* best_beam_branch, int* best_t_history, int* status,
+                                  void* stream) {
   LatticeDecodeArgs a{};
   a.B = batch_size; a.T = max_steps; a.U = max_pos; a.W = beam_width;
   a.lattice = lattice; a.input_length = input_length;
@@ -620,6 +637,49 @@ int ssnt_lattice_beam_search_decode_device(const float* lattice, const int* inpu
   a.next_fin = next_is_finished; a.beam_branch = beam_branch;
   a.best_beam_branch = best_beam_branch; a.best_t_history = best_t_history; a.status = status;
   return launch_lattice_decode(a, as_stream(stream));
+}
+
+int ssnt_v2_lattice_beam_search_decode_device(
+    const float* logits, const int* duration_table, const int* input_length,
+    const int* output_length, int batch_size, int max_steps, int beam_width,
+    int duration_class_size, int zero_duration_id, bool allow_skip, bool test_mode,
+    int* prediction, float* log_probs, int* next_t, int* next_u, bool* next_is_finished,
+    int* next_total_duration, int* beam_branch, int* ordered_beam_branch, int* path_prediction,
+    int* duration, int* status, void* stream) {
+  if (!logits || !duration_table || !input_length || !output_length || !prediction ||
+      !log_probs || !next_t || !next_u || !next_is_finished || !next_total_duration ||
+      !beam_branch || duration_class_size <= 0)
+    return SSNT_ERR_INVALID_ARG;
+  FusedDecodeArgs a{};
+  a.variant = Variant::V2;
+  a.B = batch_size; a.T = max_steps; a.W = beam_width; a.C = duration_class_size;
+  a.src = logits; a.table = duration_table;
+  a.input_length = input_length; a.output_length = output_length;
+  a.special_id = zero_duration_id; a.allow_skip = allow_skip; a.test_mode = test_mode;
+  a.prediction = prediction; a.log_prob = log_probs; a.next_t = next_t; a.next_u = next_u;
+  a.next_fin = next_is_finished; a.next_total = next_total_duration; a.beam_branch = beam_branch;
+  a.ordered = ordered_beam_branch; a.path_pred = path_prediction; a.duration = duration;
+  a.status = status;
+  return launch_fused_decode(a, as_stream(stream));
+}
+
+int ssnt_tone_latent_lattice_beam_search_decode_device(
+    const float* logits, const int* input_length, int batch_size, int max_steps, int beam_width,
+    int tone_class_size, int empty_tone_id, int* prediction, float* log_probs, int* next_t,
+    int* next_u, bool* next_is_finished, int* beam_branch, int* ordered_beam_branch,
+    int* path_prediction, int* status, void* stream) {
+  if (!logits || !input_length || !prediction || !log_probs || !next_t || !next_u ||
+      !next_is_finished || !beam_branch || tone_class_size <= 0)
+    return SSNT_ERR_INVALID_ARG;
+  FusedDecodeArgs a{};
+  a.variant = Variant::Tone;
+  a.B = batch_size; a.T = max_steps; a.W = beam_width; a.C = tone_class_size;
+  a.src = logits; a.input_length = input_length; a.special_id = empty_tone_id;
+  a.prediction = prediction; a.log_prob = log_probs; a.next_t = next_t; a.next_u = next_u;
+  a.next_fin = next_is_finished; a.beam_branch = beam_branch;
+  a.ordered = ordered_beam_branch; a.path_pred = path_prediction;
+  a.status = status;
+  return launch_fused_decode(a, as_stream(stream));
 }
 
 int ssnt_extract_best_beam_branch_device(const int* best_final_branch, const int* beam_branch,

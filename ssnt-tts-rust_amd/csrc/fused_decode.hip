@@ -1,0 +1,486 @@
+// fused_decode.hip -- the whole T-step beam-search decode of one utterance in one wave, for the
+// v1 emit/shift lattice (BASELINE configs[2]) and the v2 duration-class and tone-latent paths
+// (configs[4]), plus the backtrace of the final slots in the same launch.
+//
+// Step contract: the reference's per-step kernels, bit-exact (src/lib.rs:149-230,
+// src/v2.rs:269-339, src/tone_latent.rs:184-234). n = W*C candidates.
+//
+//   n <= 64  k_fused_reg: one candidate per lane; only the sort keys and the staged outputs touch
+//            LDS.
+//     rank     #{j : key_j > key_c} with key = (sortable(lp), 63 - c): the stable descending sort
+//              of src/lib.rs:161 (ties keep generation order), over broadcast LDS reads
+//     sort     ds_permute of the packed candidate fields to lane = rank
+//     dedup    compare with the DPP-shifted left neighbour (src/lib.rs:162, eq_ignore_parent)
+//     diagonal ballot of the kept on-diagonal lanes (src/v2.rs:283-308)
+//     pad      each candidate lane fetches (ds_bpermute) the result slot its own beam index names
+//              (cyclic pad src/lib.rs:163-167): the next step's beam state arrives in exactly the
+//              lanes that expand that beam next.
+//   n > 64   k_fused_lds: the one-wave LDS step of decode_dev.h in a loop.
+//
+// Step s's input row does not depend on the beam state (v2/tone: logits[b,s]; v1: every live
+// beam has u == s, so its row is lattice[b,s]); rows are prefetched kAhead steps ahead.
+#include <hip/hip_runtime.h>
+
+#include "decode_dev.h"
+
+namespace ssnt {
+namespace {
+
+using namespace dec;
+
+constexpr int kAhead = 4;    // input rows in flight
+constexpr int kV1Regs = 4;   // v1 lattice row floats per lane: the row is staged while 2U <= 256
+constexpr int kChunk = 32;   // per-step outputs staged in LDS and flushed every kChunk steps
+constexpr int kRing = 7;     // staged output arrays
+
+// IEEE total order of the reference's comparison (src/lib.rs:161): -0 and +0 compare equal, so
+// both map to one key. NaN is outside the parity contract.
+__device__ __forceinline__ unsigned sortable(float x) {
+  const unsigned bits = x == 0.0f ? 0u : __float_as_uint(x);
+  return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+}
+
+// One wave per workgroup: LDS operations of a wave complete in order, so a write followed by a
+// read of the same location needs no barrier -- only the compiler must keep the order.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// LDS layout of k_fused_reg (bytes), shared with the host launcher.
+struct RegLayout {
+  size_t ring, hist, row, total;
+  __host__ __device__ RegLayout(Variant v, int W, int T, int U, bool hist_lds, bool staged) {
+    ring = 512;                                              // 64 sort keys (u64)
+    hist = ring + (size_t)kRing * kChunk * W * 4;
+    const int nh = v == Variant::V2 ? 3 : 2;
+    row = hist + (hist_lds ? (size_t)nh * T * W * 4 : 0);
+    total = row + ((v == Variant::V1 && staged) ? (size_t)U * 2 * 4 : 0);
+  }
+};
+
+template <Variant V, bool STAGED>
+__global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool kV1 = V == Variant::V1, kV2 = V == Variant::V2;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int W = a.W, T = a.T, U = a.U;
+  const int C = kV1 ? 2 : a.C;
+  const int n = W * C;
+  const RegLayout L(V, W, T, U, hist_lds != 0, STAGED);
+  u64* keys = reinterpret_cast<u64*>(smem);
+  int* ring = reinterpret_cast<int*>(smem + L.ring);
+  const int RW = kChunk * W;
+  int* r_pred = ring;
+  float* r_lp = reinterpret_cast<float*>(ring + RW);
+  int* r_nt = ring + 2 * RW;
+  int* r_nu = ring + 3 * RW;
+  int* r_fin = ring + 4 * RW;
+  int* r_tot = ring + 5 * RW;
+  int* r_br = ring + 6 * RW;
+  int* h_br = reinterpret_cast<int*>(smem + L.hist);  // (T,W) parent slot
+  int* h_aux = h_br + (size_t)T * W;                   // (T,W) v1: next_t; v2/tone: prediction
+  int* h_tot = h_aux + (size_t)T * W;                  // (T,W) v2: next_total_duration
+  float* rowbuf = reinterpret_cast<float*>(smem + L.row);
+
+  const u64 I = as_usize(a.input_length[b]);
+  const u64 O = kV2 ? as_usize(a.output_length[b]) : 0;
+  const bool is_cand = lane < n;
+  const int w = is_cand ? lane / C : 0;  // the beam this lane expands (generation order w*C + i)
+  const int i = is_cand ? lane - w * C : 0;
+  const int sid = a.special_id;
+  // prediction code: class index, or C for the "not defined" padding candidate whose prediction
+  // is the special id (equal to class sid when sid names a class: eq_ignore_parent compares it)
+  const int scode = kV1 ? 0 : ((sid >= 0 && sid < C) ? sid : C);
+  const int dur = (kV2 && is_cand) ? a.table[i] : 0;
+  // v2 band constants, f32 as in total_duration_bounds (src/v2.rs:94-104)
+  const float o_over_i = (float)O / (float)I;
+  const float upper_range = (float)O * 0.1f;
+  const float lower_range = (float)O * 0.05f;
+
+  // state of beam w, replicated in its C candidate lanes
+  float hist = 0.0f;
+  int bt = 0, bu = 0, bfin = 0, btot = 0;
+
+  const int row_len = kV1 ? 2 * U : n;
+  const float* src = a.src + (size_t)b * T * row_len;
+  constexpr int R = kV1 ? kV1Regs : 1;
+  float pre[kAhead][R];
+  // unconditional (clamped) loads: a conditional load becomes a branch whose join waits for it
+  auto load_row = [&](int s, float* dst) {
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+      dst[q] = src[(size_t)min(s, T - 1) * row_len + min(lane + 64 * q, row_len - 1)];
+  };
+  if constexpr (!kV1 || STAGED) {
+#pragma unroll
+    for (int k = 0; k < kAhead; ++k) load_row(k, pre[k]);
+  }
+
+  auto flush = [&](int s0, int steps) {  // staged outputs of steps [s0, s0+steps), coalesced
+    lds_order();
+    const int cnt = steps * W;
+    const size_t g0 = ((size_t)b * T + s0) * W;
+    for (int k = lane; k < cnt; k += 64) {
+      a.prediction[g0 + k] = r_pred[k];
+      a.log_prob[g0 + k] = r_lp[k];
+      a.next_t[g0 + k] = r_nt[k];
+      a.next_u[g0 + k] = r_nu[k];
+      a.next_fin[g0 + k] = r_fin[k] != 0;
+      a.beam_branch[g0 + k] = r_br[k];
+      if constexpr (kV2) a.next_total[g0 + k] = r_tot[k];
+    }
+    lds_order();
+  };
+
+  // one step; false when v2 finds no candidate (src/v2.rs:292)
+  auto step = [&](int s, float* row) -> bool {
+    if constexpr (kV1 && STAGED) {  // row s to LDS, then row s + kAhead into the freed registers
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const int idx = lane + 64 * q;
+        if (idx < row_len) rowbuf[idx] = row[q];
+      }
+      load_row(s + kAhead, row);
+      lds_order();
+    }
+    // ---- candidate of this lane (decode_dev.h gen_candidate, one lane per candidate)
+    const bool defined = !bfin && as_usize(bt) < I;
+    int valid, code, nt, nu, fin, tot = btot;
+    float lp;
+    if (!defined) {  // "End of input. Return values to fill padding region."
+      valid = i == 0; code = scode; lp = hist; nt = bt; nu = bu; fin = 1;
+    } else if constexpr (kV1) {  // src/lib.rs:186-227
+      const bool hdef = (unsigned)bu < (unsigned)T && (unsigned)bt < (unsigned)U;
+      float hv = 0.0f;
+      if (is_cand && hdef) {
+        if constexpr (STAGED) hv = rowbuf[2 * bt + i];  // bu == s for every live beam
+        else hv = src[((size_t)bu * U + bt) * 2 + i];
+      }
+      const bool last = as_usize(bt) == I - 1;
+      valid = 1;
+      if (i == 0 && last) { code = 0; lp = hist + hv; nt = bt; nu = bu; fin = 1; }
+      else if (i == 1 && last) { code = 0; lp = hist; nt = bt; nu = bu; fin = 1; }  // prohibited shift
+      else if (i == 1) { code = 1; lp = hist + hv; nt = bt + 1; nu = bu + 1; fin = 0; }
+      else { code = 0; lp = hist + hv; nt = bt; nu = bu + 1; fin = 0; }
+    } else if constexpr (V == Variant::Tone) {  // src/tone_latent.rs:87-93, 220-231
+      valid = 1; code = i; lp = hist + row[0]; nt = bt + 1; nu = bu + 1; fin = 0;
+    } else {  // v2: src/v2.rs:119-166, 326-336
+      tot = (int)((unsigned)btot + (unsigned)dur);
+      const u64 t = as_usize(bt);
+      const float diagonal = o_over_i * (float)(t + 1);
+      const int lb = f2i_sat(fmaxf(diagonal - lower_range, 0.0f));
+      const int ub = f2i_sat(fminf(diagonal + upper_range, (float)O));
+      const bool overrun = (I - (t + 1)) * 3 > O;
+      bool f = false, ok = true;
+      if (!a.test_mode && (tot < lb || tot > ub)) ok = false;
+      else if (!a.test_mode && overrun) ok = false;
+      else if (t == I - 1) {
+        if (!a.test_mode && tot != (int)O) ok = false;
+        else if (!a.allow_skip && i == sid) ok = false;
+        else f = true;
+      } else if (!a.allow_skip && i == sid) ok = false;
+      valid = ok; code = i; lp = hist + row[0];
+      nt = f ? bt : bt + 1; nu = f ? bu : bu + 1; fin = f;
+    }
+    if constexpr (!kV1) load_row(s + kAhead, row);
+    valid = valid && is_cand;
+    // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
+    const u64 key = ((u64)(valid ? sortable(lp) : 0u) << 32) | (unsigned)(63 - lane);
+    keys[lane] = key;
+    lds_order();
+    int rank = 0;
+    const int n2 = (n + 1) & ~1;
+    for (int j = 0; j < n2; j += 2) {
+      const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(keys + j);  // broadcast read
+      rank += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
+    }
+    lds_order();
+    const u64 vmask = __ballot(valid);
+    const int nvalid = __popcll(vmask);
+    const u64 below = (1ull << lane) - 1ull;
+    // a full permutation of the 64 lanes: valid candidates to their rank, the rest after them
+    const int dst = valid ? rank : nvalid + __popcll(~vmask & below);
+    const int pk = code | (fin << 7) | (w << 8);
+    const int ntu = (nt << 16) | (nu & 0xffff);
+    const int s_lp = perm_i(dst, __float_as_int(lp));
+    const int s_ntu = perm_i(dst, ntu);
+    const int s_pk = perm_i(dst, pk);
+    const int s_tot = kV2 ? perm_i(dst, tot) : 0;
+    // ---- consecutive dedup, keep the first of each run (src/lib.rs:162; v2 adds the total)
+    // every cross-lane read happens with the whole wave active: a DPP read of a lane that is
+    // off in the exec mask returns the old value, so no shift may sit behind a short circuit
+    const int p_lp = wave_shr1(s_lp), p_ntu = wave_shr1(s_ntu), p_pk = wave_shr1(s_pk);
+    const int p_tot = kV2 ? wave_shr1(s_tot) : 0;
+    const bool same = (((s_pk ^ p_pk) & 0xff) == 0) & (__int_as_float(s_lp) == __int_as_float(p_lp)) &
+                      (s_ntu == p_ntu) & (s_tot == p_tot);
+    const bool keep = lane < nvalid && (lane == 0 || !same);
+    const u64 kmask = __ballot(keep);
+    const int nkept = __popcll(kmask);
+    if (nkept == 0) return false;  // v2 only: assert_ne!(n_results, 0) (src/v2.rs:292)
+    // ---- v2 diagonal injection (src/v2.rs:283-308): first kept candidate on the diagonal
+    int dk = -1;
+    if constexpr (kV2) {
+      if (!a.test_mode) {
+        const float diag = o_over_i * (float)(u64)((unsigned)s_ntu >> 16);
+        const float diff = (float)s_tot - diag;
+        const u64 dmask = __ballot(keep && diff >= -20.0f && diff <= 0.0f);
+        if (dmask) dk = __popcll(kmask & ((1ull << (__ffsll((long long)dmask) - 1)) - 1ull));
+      }
+    }
+    // ---- compaction (kept element k -> its sorted lane) and the cyclic pad
+    const int cdst = keep ? __popcll(kmask & below) : nkept + __popcll(~kmask & below);
+    const int kl = perm_i(cdst, lane);
+    const int k = (dk >= 0 && w == W - 1) ? dk : (w < nkept ? w : w % nkept);
+    const int srcl = bperm_i(k, kl);
+    const int g_lp = bperm_i(srcl, s_lp), g_ntu = bperm_i(srcl, s_ntu), g_pk = bperm_i(srcl, s_pk);
+    const int g_tot = kV2 ? bperm_i(srcl, s_tot) : 0;
+    hist = __int_as_float(g_lp);
+    bt = (int)((unsigned)g_ntu >> 16);
+    bu = g_ntu & 0xffff;
+    bfin = (g_pk >> 7) & 1;
+    btot = g_tot;
+    // ---- outputs of slot w (src/lib.rs:138-145), staged
+    const int cs = s % kChunk;
+    if (is_cand && i == 0) {
+      const int pc = g_pk & 0x7f;
+      const int pred = pc == C ? sid : pc;
+      const int parent = g_pk >> 8;
+      const int o = cs * W + w;
+      r_pred[o] = pred; r_lp[o] = hist; r_nt[o] = bt; r_nu[o] = bu; r_fin[o] = bfin;
+      r_br[o] = parent;
+      if constexpr (kV2) r_tot[o] = btot;
+      if (hist_lds) {
+        const int hs = s * W + w;
+        h_br[hs] = parent;
+        h_aux[hs] = kV1 ? bt : pred;
+        if constexpr (kV2) h_tot[hs] = btot;
+      }
+    }
+    if (cs == kChunk - 1 || s == T - 1) flush(s - cs, cs + 1);
+    return true;
+  };
+
+  bool ok = true;
+  for (int s0 = 0; s0 < T && ok; s0 += kAhead) {  // unrolled by the ring: register indices fixed
+#pragma unroll
+    for (int k = 0; k < kAhead; ++k)
+      if (ok && s0 + k < T) ok = step(s0 + k, pre[k]);
+  }
+  if (!ok) {
+    if (lane == 0 && a.status) atomicOr(a.status, kStatusNoCandidate);
+    return;
+  }
+  if (!hist_lds) return;  // the host runs k_fused_paths over the global outputs
+  // ---- backtrace of final slot `lane` (v2_util.rs:6-36 with final_branch = [0..W); util.rs:20-33
+  // for slot 0 with t history = next_t)
+  lds_order();
+  if (lane < W) {
+    int cur = lane;
+    int* ord = a.ordered ? a.ordered + ((size_t)b * W + lane) * T : nullptr;
+    int* pp = a.path_pred ? a.path_pred + ((size_t)b * W + lane) * T : nullptr;
+    int* du = a.duration ? a.duration + ((size_t)b * W + lane) * T : nullptr;
+    const bool best = lane == 0 && a.best_beam_branch;
+    for (int s = T - 1; s >= 0; --s) {
+      const int hs = s * W + cur;
+      const int parent = h_br[hs];
+      if (ord) ord[s] = cur;
+      if constexpr (!kV1) {
+        if (pp) pp[s] = h_aux[hs];
+      }
+      if constexpr (kV2) {
+        if (du) du[s] = h_tot[hs] - (s > 0 ? h_tot[hs - W - cur + parent] : 0);
+      }
+      if (best) {
+        a.best_beam_branch[(size_t)b * T + s] = cur;
+        a.best_t_history[(size_t)b * T + s] = h_aux[hs];
+      }
+      cur = parent;
+    }
+  }
+}
+
+// Any n: the one-wave LDS step (decode_dev.h step_wave) in a loop; beam state in LDS.
+template <Variant V>
+__global__ __launch_bounds__(64) void k_fused_lds(FusedDecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool kV1 = V == Variant::V1;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int W = a.W, T = a.T, U = a.U;
+  const int C = kV1 ? 2 : a.C;
+  const int n = W * C;
+  Cand* cand = reinterpret_cast<Cand*>(smem);
+  int* order = reinterpret_cast<int*>(cand + n);
+  int* kept = order + n;
+  float* st_hist = reinterpret_cast<float*>(kept + n);  // (W) state, then (W) next state
+  int* st_t = reinterpret_cast<int*>(st_hist + 2 * W);
+  int* st_u = st_t + 2 * W;
+  int* st_tot = st_u + 2 * W;
+  float* hbuf = reinterpret_cast<float*>(st_tot + 2 * W);  // (W,2) v1 inputs
+  bool* st_fin = reinterpret_cast<bool*>(hbuf + (kV1 ? 2 * W : 0));  // (2W)
+  StepArgs sa{};
+  sa.variant = V;
+  sa.B = a.B; sa.W = W; sa.Wmax = W; sa.C = C;
+  sa.table = a.table; sa.special_id = kV1 ? 0 : a.special_id;
+  sa.allow_skip = a.allow_skip; sa.test_mode = a.test_mode;
+  BatchView v;
+  v.hist = st_hist; v.fin = st_fin; v.t = st_t; v.u = st_u; v.total = st_tot;
+  v.I = as_usize(a.input_length[b]);
+  v.O = V == Variant::V2 ? as_usize(a.output_length[b]) : 0;
+  const int row_len = kV1 ? 2 * U : n;
+  const float* src = a.src + (size_t)b * T * row_len;
+  for (int x = lane; x < W; x += 64) {
+    st_hist[x] = 0.0f; st_t[x] = 0; st_u[x] = 0; st_tot[x] = 0; st_fin[x] = false;
+  }
+  __syncthreads();
+  for (int s = 0; s < T; ++s) {
+    if constexpr (kV1) {
+      for (int x = lane; x < W; x += 64) {
+        const bool hdef = !st_fin[x] && as_usize(st_t[x]) < v.I && (unsigned)st_u[x] < (unsigned)T &&
+                          (unsigned)st_t[x] < (unsigned)U;
+        float2 h = make_float2(0.0f, 0.0f);
+        if (hdef) h = *reinterpret_cast<const float2*>(src + ((size_t)st_u[x] * U + st_t[x]) * 2);
+        hbuf[2 * x] = h.x;
+        hbuf[2 * x + 1] = h.y;
+      }
+      v.h = hbuf;
+      __syncthreads();
+    } else {
+      v.h = src + (size_t)s * row_len;
+    }
+    const size_t o = ((size_t)b * T + s) * W;
+    const int nk = step_wave(sa, v, cand, order, kept, W, [&](int x, const Cand& r) {
+      a.prediction[o + x] = r.pred;
+      a.log_prob[o + x] = r.lp;
+      a.next_t[o + x] = (int)(unsigned)r.nt;
+      a.next_u[o + x] = (int)(unsigned)r.nu;
+      a.next_fin[o + x] = r.fin != 0;
+      a.beam_branch[o + x] = r.parent;
+      if (V == Variant::V2) a.next_total[o + x] = r.tot;
+      st_hist[W + x] = r.lp;
+      st_t[W + x] = (int)(unsigned)r.nt;
+      st_u[W + x] = (int)(unsigned)r.nu;
+      st_tot[W + x] = r.tot;
+      st_fin[W + x] = r.fin != 0;
+    });
+    if (nk == 0) {
+      if (lane == 0 && a.status) atomicOr(a.status, kStatusNoCandidate);
+      return;
+    }
+    __syncthreads();
+    for (int x = lane; x < W; x += 64) {
+      st_hist[x] = st_hist[W + x]; st_t[x] = st_t[W + x]; st_u[x] = st_u[W + x];
+      st_tot[x] = st_tot[W + x]; st_fin[x] = st_fin[W + x];
+    }
+    __syncthreads();
+  }
+}
+
+// Backtrace over the global per-step outputs, one thread per (utterance, final slot): the path
+// outputs of k_fused_lds, and of k_fused_reg when its history does not fit LDS.
+__global__ __launch_bounds__(64) void k_fused_paths(FusedDecodeArgs a) {
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  const int W = a.W, T = a.T;
+  if (id >= a.B * W) return;
+  const int b = id / W, w = id - b * W;
+  int* ord = a.ordered ? a.ordered + ((size_t)b * W + w) * T : nullptr;
+  int* pp = a.path_pred ? a.path_pred + ((size_t)b * W + w) * T : nullptr;
+  int* du = a.duration ? a.duration + ((size_t)b * W + w) * T : nullptr;
+  const bool best = w == 0 && a.best_beam_branch;
+  bool bad = false;
+  int cur = w;
+  for (int s = T - 1; s >= 0; --s) {
+    const size_t o = ((size_t)b * T + s) * W;
+    int parent = a.beam_branch[o + cur];
+    if (parent < 0 || parent >= W) {  // only after "no candidate" left this utterance unwritten
+      bad = true;
+      parent = 0;
+    }
+    if (ord) ord[s] = cur;
+    if (pp) pp[s] = a.prediction[o + cur];
+    if (du) du[s] = a.next_total[o + cur] - (s > 0 ? a.next_total[o - W + parent] : 0);
+    if (best) {
+      a.best_beam_branch[(size_t)b * T + s] = cur;
+      a.best_t_history[(size_t)b * T + s] = a.next_t[o + cur];
+    }
+    cur = parent;
+  }
+  if (bad && a.status) atomicOr(a.status, kStatusBadIndex);
+}
+
+inline int last_error() { return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP; }
+
+constexpr size_t kMaxLds = 150 * 1024;
+
+template <typename K>
+int launch_with_lds(K kernel, size_t lds, int B, hipStream_t st, const FusedDecodeArgs& a,
+                    int extra) {
+  if (lds > 64 * 1024)  // per launch: the attribute is per device, and cheap to set
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
+  hipLaunchKernelGGL(kernel, dim3(B), dim3(64), lds, st, a, extra);
+  return last_error();
+}
+
+template <Variant V>
+int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
+  const int C = V == Variant::V1 ? 2 : a.C;
+  const int n = a.W * C;
+  const bool want_paths = a.ordered || a.path_pred || a.duration || a.best_beam_branch;
+  bool paths_kernel = want_paths;
+  int rc;
+  if (n <= 64) {
+    const bool staged = V != Variant::V1 || 2 * (size_t)a.U <= 64 * (size_t)kV1Regs;
+    const bool hist_lds = RegLayout(V, a.W, a.T, a.U, true, staged).total <= kMaxLds;
+    const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged).total;
+    if (lds > kMaxLds) return SSNT_ERR_UNSUPPORTED;
+    if (staged) rc = launch_with_lds(k_fused_reg<V, true>, lds, a.B, st, a, hist_lds ? 1 : 0);
+    else if constexpr (V == Variant::V1)  // only v1 rows can be too long to stage
+      rc = launch_with_lds(k_fused_reg<V, false>, lds, a.B, st, a, hist_lds ? 1 : 0);
+    paths_kernel = want_paths && !hist_lds;
+  } else {
+    const size_t lds = (size_t)n * sizeof(Cand) + 2 * (size_t)n * 4 + (size_t)a.W * 2 * 16 +
+                       (V == Variant::V1 ? (size_t)a.W * 8 : 0) + 2 * (size_t)a.W + 16;
+    if (lds > kMaxLds) return SSNT_ERR_UNSUPPORTED;
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_fused_lds<V>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
+    hipLaunchKernelGGL(k_fused_lds<V>, dim3(a.B), dim3(64), lds, st, a);
+    rc = last_error();
+  }
+  if (rc != SSNT_OK || !paths_kernel) return rc;
+  const int threads = a.B * a.W;
+  hipLaunchKernelGGL(k_fused_paths, dim3((threads + 63) / 64), dim3(64), 0, st, a);
+  return last_error();
+}
+
+}  // namespace
+
+int launch_fused_decode(const FusedDecodeArgs& a, hipStream_t st) {
+  if (a.B < 0 || a.W <= 0 || a.T <= 0 || !a.src || !a.input_length || !a.prediction ||
+      !a.log_prob || !a.next_t || !a.next_u || !a.next_fin || !a.beam_branch)
+    return SSNT_ERR_INVALID_ARG;
+  // packed (next_t, next_u) in 16 bits each: every value stays <= T in a fused decode
+  if (a.T > 32767) return SSNT_ERR_UNSUPPORTED;
+  if ((a.best_beam_branch == nullptr) != (a.best_t_history == nullptr)) return SSNT_ERR_INVALID_ARG;
+  switch (a.variant) {
+    case Variant::V1:
+      if (a.U <= 0 || a.C != 2 || a.path_pred || a.duration) return SSNT_ERR_INVALID_ARG;
+      if (a.W > 64) return SSNT_ERR_UNSUPPORTED;
+      break;
+    case Variant::V2:
+      if (a.C <= 0 || !a.table || !a.output_length || !a.next_total) return SSNT_ERR_INVALID_ARG;
+      if (a.best_beam_branch) return SSNT_ERR_INVALID_ARG;
+      break;
+    case Variant::Tone:
+      if (a.C <= 0 || a.duration || a.best_beam_branch) return SSNT_ERR_INVALID_ARG;
+      break;
+  }
+  if (a.B == 0) return SSNT_OK;
+  switch (a.variant) {
+    case Variant::V1: return launch_variant<Variant::V1>(a, st);
+    case Variant::V2: return launch_variant<Variant::V2>(a, st);
+    default: return launch_variant<Variant::Tone>(a, st);
+  }
+}
+
+}  // namespace ssnt

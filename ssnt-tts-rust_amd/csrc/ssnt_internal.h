@@ -92,6 +92,39 @@ struct LatticeDecodeArgs {
 };
 int launch_lattice_decode(const LatticeDecodeArgs& a, hipStream_t stream);
 
+// Fused multi-step decode (fused_decode.hip): all beams start at t = u = 0, log-prob 0,
+// total 0, not finished; step s feeds the exact per-step contract with
+//   V1:        h[w] = src[b, s, t_w, :]  (src = (B,T,U,2) lattice; live beams have u_w == s)
+//   V2 / Tone: h    = src[b, s]          (src = (B,T,W,C) per-step logits)
+// and the step's outputs become the next state (the role of the TF decode loop). After the
+// last step the final slots are backtraced in the same launch.
+struct FusedDecodeArgs {
+  Variant variant;
+  int B, T, U, W, C;         // U: lattice positions (V1 only); C: classes (2 for V1)
+  const float* src;
+  const int* table;          // (C) v2 duration_table
+  const int* input_length;   // (B)
+  const int* output_length;  // (B) v2
+  int special_id;            // v2 zero_duration_id / tone empty_tone_id (v1: 0)
+  bool allow_skip, test_mode;
+  // per-step outputs (B,T,W)
+  int* prediction;
+  float* log_prob;
+  int* next_t;
+  int* next_u;
+  bool* next_fin;
+  int* next_total;           // v2 (required)
+  int* beam_branch;
+  // path outputs, each optional
+  int* ordered;              // (B,W,T): order_beam_branch with final_branch = [0..W)
+  int* path_pred;            // (B,W,T): prediction along each path
+  int* duration;             // (B,W,T): v2 duration added at each step of each path
+  int* best_beam_branch;     // (B,T): path of slot 0 (util.rs:20-33)
+  int* best_t_history;       // (B,T): next_t along that path
+  int* status;
+};
+int launch_fused_decode(const FusedDecodeArgs& a, hipStream_t stream);
+
 int launch_extract_best(int B, int W, int U, const int* best_final_branch, const int* beam_branch,
                         const int* t_history, int* best_beam_branch, int* best_t_history,
                         int* status, hipStream_t stream);

@@ -26,7 +26,8 @@ __all__ = [
     "beam_search_decode", "extract_best_beam_branch", "ssnt_tts_v2_beam_search_decode",
     "order_beam_branch", "upsample_source_indexes", "tone_latent_beam_search_decode",
     "levenshtein_edit_distance", "ssnt_fwd_bwd", "SSNTLatticeLoss", "ssnt_lattice_loss",
-    "lattice_beam_search_decode", "SsntError", "FLAG_TERMINAL_EMIT", "FLAG_ZERO_INFINITY",
+    "lattice_beam_search_decode", "v2_lattice_beam_search_decode",
+    "tone_latent_lattice_beam_search_decode", "SsntError", "FLAG_TERMINAL_EMIT", "FLAG_ZERO_INFINITY",
 ]
 
 
@@ -390,4 +391,74 @@ def lattice_beam_search_decode(lattice, input_length, beam_width, *, check=True)
         _p(o["next_u"]), _p(o["next_is_finished"]), _p(o["beam_branch"]),
         _p(o["best_beam_branch"]), _p(o["best_t_history"]), _p(st), _stream(dev))
     _finish("lattice_beam_search_decode", rc, st, check)
+    return o
+
+
+_STEP_OUTS = (("prediction", torch.int32), ("log_prob", torch.float32), ("next_t", torch.int32),
+              ("next_u", torch.int32), ("next_is_finished", torch.bool))
+
+
+def v2_lattice_beam_search_decode(logits, duration_table, input_length, output_length,
+                                  beam_width, zero_duration_id, allow_skip, test_mode, *,
+                                  upsample=False, out_of_range_source_index=-1, check=True):
+    """Fused multi-step v2 decode over per-step logits (B,T,W,D): every beam starts at
+    t = u = 0, log-prob 0, total 0; step s runs the ssnt_tts_v2_beam_search_decode step
+    (src/v2.rs:221-339) on h = logits[:, s] and feeds its outputs back as the next state, all in
+    one launch. Returns the per-step outputs (B,T,W) under the reference op's output names,
+    plus ordered_beam_branch / path_prediction / duration (B,W,T) of every final slot
+    (src/v2_util.rs:6-36). upsample=True adds upsampled_source_indexes (B,W,max total) from the
+    durations and each slot's final total (src/v2_util.rs:39-66)."""
+    lib = load(require_gpu=True)
+    lg = _dev(logits, torch.float32, "logits")
+    dev = lg.device
+    B, T, W, D = lg.shape
+    if W != beam_width:
+        raise ValueError("logits must be (B, T, beam_width, duration_class_size)")
+    table = _dev(duration_table, torch.int32, "duration_table").reshape(D)
+    il = _dev(input_length, torch.int32, "input_length").reshape(B)
+    # the reference wrapper zeroes output_length in test mode (__init__.py:47)
+    ol = torch.zeros_like(il) if test_mode else _dev(output_length, torch.int32,
+                                                     "output_length").reshape(B)
+    o = {k: torch.empty((B, T, W), dtype=dt, device=dev) for k, dt in _STEP_OUTS}
+    o["next_total_duration"] = torch.empty((B, T, W), dtype=torch.int32, device=dev)
+    o["beam_branch"] = torch.empty((B, T, W), dtype=torch.int32, device=dev)
+    for k in ("ordered_beam_branch", "path_prediction", "duration"):
+        o[k] = torch.empty((B, W, T), dtype=torch.int32, device=dev)
+    st = _status(dev)
+    rc = lib.ssnt_v2_lattice_beam_search_decode_device(
+        _p(lg), _p(table), _p(il), _p(ol), B, T, W, D, int(zero_duration_id), bool(allow_skip),
+        bool(test_mode), _p(o["prediction"]), _p(o["log_prob"]), _p(o["next_t"]), _p(o["next_u"]),
+        _p(o["next_is_finished"]), _p(o["next_total_duration"]), _p(o["beam_branch"]),
+        _p(o["ordered_beam_branch"]), _p(o["path_prediction"]), _p(o["duration"]), _p(st),
+        _stream(dev))
+    _finish("v2_lattice_beam_search_decode", rc, st, check)
+    if upsample:
+        o["upsampled_source_indexes"] = upsample_source_indexes(
+            o["duration"], o["next_total_duration"][:, -1, :], out_of_range_source_index, W,
+            check=check)
+    return o
+
+
+def tone_latent_lattice_beam_search_decode(logits, input_length, beam_width, empty_tone_id, *,
+                                           check=True):
+    """Fused multi-step tone-latent decode over per-step logits (B,T,W,C): the
+    tone_latent_beam_search_decode step (src/tone_latent.rs:144-234) T times in one launch.
+    Returns the per-step outputs (B,T,W) plus ordered_beam_branch / path_prediction (B,W,T)."""
+    lib = load(require_gpu=True)
+    lg = _dev(logits, torch.float32, "logits")
+    dev = lg.device
+    B, T, W, C = lg.shape
+    if W != beam_width:
+        raise ValueError("logits must be (B, T, beam_width, tone_class_size)")
+    il = _dev(input_length, torch.int32, "input_length").reshape(B)
+    o = {k: torch.empty((B, T, W), dtype=dt, device=dev) for k, dt in _STEP_OUTS}
+    o["beam_branch"] = torch.empty((B, T, W), dtype=torch.int32, device=dev)
+    for k in ("ordered_beam_branch", "path_prediction"):
+        o[k] = torch.empty((B, W, T), dtype=torch.int32, device=dev)
+    st = _status(dev)
+    rc = lib.ssnt_tone_latent_lattice_beam_search_decode_device(
+        _p(lg), _p(il), B, T, W, C, int(empty_tone_id), _p(o["prediction"]), _p(o["log_prob"]),
+        _p(o["next_t"]), _p(o["next_u"]), _p(o["next_is_finished"]), _p(o["beam_branch"]),
+        _p(o["ordered_beam_branch"]), _p(o["path_prediction"]), _p(st), _stream(dev))
+    _finish("tone_latent_lattice_beam_search_decode", rc, st, check)
     return o

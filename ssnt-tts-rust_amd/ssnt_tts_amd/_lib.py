@@ -50,6 +50,12 @@ SIGNATURES = {
                                                            c_int, P, P, P, P, P, P, P, P]),
     "ssnt_lattice_beam_search_decode_device": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P,
                                                        P, P, P, P, P, P, P]),
+    "ssnt_v2_lattice_beam_search_decode_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int,
+                                                          c_int, c_bool, c_bool, P, P, P, P, P, P,
+                                                          P, P, P, P, P, P]),
+    "ssnt_tone_latent_lattice_beam_search_decode_device": (c_int, [P, P, c_int, c_int, c_int,
+                                                                   c_int, c_int, P, P, P, P, P, P,
+                                                                   P, P, P, P]),
     "ssnt_extract_best_beam_branch_device": (c_int, [P, P, P, c_int, c_int, c_int, P, P, P, P]),
     "ssnt_order_beam_branch_device": (c_int, [P, P, c_int, c_int, c_int, P, P, P]),
     "ssnt_upsample_source_indexes_device": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P]),

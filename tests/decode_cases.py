@@ -74,3 +74,56 @@ def v2_case(seed):
     return dict(h=h, hist=hist, fin=fin, total=tot, table=table, t=t, u=u, input_length=I,
                 output_length=O, zero_duration_id=int(rng.integers(0, D)),
                 allow_skip=bool(rng.integers(0, 2)), test_mode=bool(rng.random() < 0.25))
+
+
+def v2_case_long(seed, W, D, B=3, I=400, O=2000):
+    """A single v2 step at the configs[4] lengths (I=400, O=2000): beams at random positions
+    with totals near the diagonal, so band / exact-length / diagonal rules all fire."""
+    rng = np.random.default_rng(seed + 3000)
+    table = np.arange(D, dtype=np.int32)
+    tie = bool(rng.integers(0, 2))
+    h = _logits(rng, (B, W, D), tie)
+    hist = _logits(rng, (B, W), True)
+    t = rng.integers(0, I, size=(B, W)).astype(np.int32)
+    if rng.random() < 0.5:
+        t[:, : max(1, W // 2)] = I - 1
+    diag = O / I * t
+    tot = np.maximum(0, diag + rng.integers(-8, 6, size=(B, W))).astype(np.int32)
+    tot[t == I - 1] = O - rng.integers(0, D, size=int((t == I - 1).sum()))
+    u = t.copy()
+    fin = rng.random((B, W)) < 0.1
+    return dict(h=h, hist=hist, fin=fin, total=tot, table=table, t=t, u=u,
+                input_length=np.full(B, I, np.int32), output_length=np.full(B, O, np.int32),
+                zero_duration_id=0, allow_skip=bool(rng.integers(0, 2)),
+                test_mode=bool(rng.random() < 0.25))
+
+
+def fused_v2_case(seed):
+    """Small fused v2 decode: per-step logits (B,T,W,D), ragged I <= T, O >= 3(I-1)."""
+    rng = np.random.default_rng(seed + 4000)
+    B, W, D = int(rng.integers(1, 5)), int(rng.integers(1, 6)), int(rng.integers(2, 10))
+    if rng.random() < 0.3:  # more candidates than lanes: the any-size kernel
+        W, D = int(rng.integers(5, 9)), int(rng.integers(14, 20))
+    T = int(rng.integers(1, 24))
+    I = rng.integers(1, T + 1, size=B).astype(np.int32)
+    O = (3 * np.maximum(I - 1, 0) + rng.integers(0, 3 * D, size=B)).astype(np.int32)
+    tie = bool(rng.integers(0, 2))
+    logits = _logits(rng, (B, T, W, D), tie)
+    table = np.arange(D, dtype=np.int32)
+    if rng.random() < 0.3:
+        table = rng.integers(0, D + 3, size=D).astype(np.int32)
+    return dict(logits=logits, table=table, input_length=I, output_length=O,
+                zero_duration_id=int(rng.integers(-1, D + 1)), allow_skip=bool(rng.integers(0, 2)),
+                test_mode=bool(rng.random() < 0.3))
+
+
+def fused_tone_case(seed):
+    rng = np.random.default_rng(seed + 5000)
+    B, W, C = int(rng.integers(1, 5)), int(rng.integers(1, 8)), int(rng.integers(1, 8))
+    if rng.random() < 0.25:
+        W, C = int(rng.integers(10, 17)), int(rng.integers(5, 9))
+    T = int(rng.integers(1, 24))
+    I = rng.integers(0, T + 2, size=B).astype(np.int32)
+    tie = bool(rng.integers(0, 2))
+    return dict(logits=_logits(rng, (B, T, W, C), tie), input_length=I,
+                empty_tone_id=int(rng.integers(-1, C + 1)))

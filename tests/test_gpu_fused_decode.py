@@ -1,0 +1,166 @@
+"""GPU parity of the fused multi-step decodes (BASELINE configs[4]: v2 + tone_latent at
+I=400 input positions, O=2000 frames, D=16, C=5, W=4, B=64) against the oracle's fused
+restatement, which tests/test_oracle_fused_decode.py pins to a loop of the per-step oracle.
+Bit-exact on every per-step output and every path output; "no candidate" (the reference's
+panic, src/v2.rs:292) must be reported for the same inputs."""
+import numpy as np
+import pytest
+import torch
+
+import decode_cases as dc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+V2_OUT = ("prediction", "log_prob", "next_t", "next_u", "next_is_finished", "next_total_duration",
+          "beam_branch", "ordered_beam_branch", "path_prediction", "duration")
+TONE_OUT = ("prediction", "log_prob", "next_t", "next_u", "next_is_finished", "beam_branch",
+            "ordered_beam_branch", "path_prediction")
+
+
+def _t(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+
+
+def _same(g, o, keys, ctx):
+    for k in keys:
+        gv = g[k].cpu().numpy()
+        if not np.array_equal(gv, o[k]):
+            bad = np.argwhere(gv != o[k])
+            raise AssertionError(f"{ctx} {k}: {len(bad)} mismatches, first at {bad[0].tolist()}")
+
+
+def _v2(gpu, oracle, lg, table, il, ol, zid, skip, test_mode, ctx, upsample=False):
+    o, rc = oracle.v2_lattice_decode(lg, table, il, ol, zid, skip, test_mode)
+    args = (_t(lg), _t(table), _t(il), _t(ol), lg.shape[2], zid, skip, test_mode)
+    if rc == 3:
+        with pytest.raises(gpu.SsntError):
+            gpu.v2_lattice_beam_search_decode(*args)
+        return None
+    assert rc == 0
+    g = gpu.v2_lattice_beam_search_decode(*args, upsample=upsample)
+    _same(g, o, V2_OUT, ctx)
+    return g, o
+
+
+def _config5(oracle, seed, B=64, I=400, O=2000, D=16, W=4, ragged=False, **kw):
+    rng = np.random.default_rng(seed)
+    if ragged:
+        Ib = rng.integers(I // 2, I + 1, size=B).astype(np.int32)
+        Ob = (Ib * (O // I) + rng.integers(-20, 21, size=B)).astype(np.int32)
+    else:
+        Ib, Ob = np.full(B, I, np.int32), np.full(B, O, np.int32)
+    d = oracle.synth_durations(B, Ib, Ob, D, seed=seed)
+    d = np.pad(d, ((0, 0), (0, I - d.shape[1])))
+    return oracle.synth_v2_logits(d, W, D, seed=seed + 100, **kw), Ib, Ob, d
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_v2_config5_full_size(gpu, oracle, seed):
+    """B=64 T=I=400 O=2000 D=16 W=4 (W*D = 64: one candidate per lane), logits peaked on a
+    sampled duration path that sums to O: the band and exact-length rules decide every step."""
+    D = 16
+    lg, il, ol, d = _config5(oracle, seed)
+    g, o = _v2(gpu, oracle, lg, np.arange(D, dtype=np.int32), il, ol, 0, False, False,
+               f"seed={seed}", upsample=True)
+    assert np.array_equal(o["path_prediction"][:, 0], d)  # the sampled path is the best beam
+    assert (o["next_total_duration"][:, -1] == 2000).all()
+    up, urc = oracle.upsample_source_indexes(o["duration"], o["next_total_duration"][:, -1], 2000)
+    assert urc == 0
+    assert np.array_equal(g["upsampled_source_indexes"].cpu().numpy(), up)
+
+
+def test_v2_config5_test_mode(gpu, oracle):
+    lg, il, ol, _ = _config5(oracle, 7)
+    _v2(gpu, oracle, lg, np.arange(16, dtype=np.int32), il, ol, 0, False, True, "test_mode")
+
+
+def test_v2_config5_tie_rich(gpu, oracle):
+    lg, il, ol, _ = _config5(oracle, 8, tie_rich=True)
+    _v2(gpu, oracle, lg, np.arange(16, dtype=np.int32), il, ol, 0, False, False, "tie-rich")
+
+
+def test_v2_config5_ragged_lengths(gpu, oracle):
+    """Per-utterance I in [200, 400] and O near 5 I: finished beams keep padding until T=400."""
+    lg, il, ol, _ = _config5(oracle, 9, ragged=True)
+    _v2(gpu, oracle, lg, np.arange(16, dtype=np.int32), il, ol, 0, False, False, "ragged")
+
+
+def test_v2_config5_allow_skip(gpu, oracle):
+    lg, il, ol, _ = _config5(oracle, 10, margin=6.0)
+    _v2(gpu, oracle, lg, np.arange(16, dtype=np.int32), il, ol, 0, True, False, "allow_skip")
+
+
+def test_v2_no_candidate_is_reported(gpu, oracle):
+    """A weak peak loses the exact-length path in some utterances: both sides report it."""
+    lg, il, ol, _ = _config5(oracle, 2, margin=2.0)
+    o, rc = oracle.v2_lattice_decode(lg, np.arange(16), il, ol, 0, False, False)
+    assert rc == 3
+    _v2(gpu, oracle, lg, np.arange(16, dtype=np.int32), il, ol, 0, False, False, "no-candidate")
+
+
+@pytest.mark.parametrize("W,D", [(5, 16), (8, 16), (3, 30)])
+def test_v2_more_candidates_than_lanes(gpu, oracle, W, D):
+    """W*D > 64: the any-size LDS kernel, at I=400 O=2000."""
+    lg, il, ol, _ = _config5(oracle, 11 + W, B=8, D=D, W=W)
+    _v2(gpu, oracle, lg, np.arange(D, dtype=np.int32), il, ol, 0, False, False, f"W={W} D={D}")
+
+
+@pytest.mark.parametrize("seed", range(150))
+def test_v2_fused_random(gpu, oracle, seed):
+    c = dc.fused_v2_case(seed)
+    _v2(gpu, oracle, c["logits"], c["table"], c["input_length"], c["output_length"],
+        c["zero_duration_id"], c["allow_skip"], c["test_mode"], f"seed={seed}")
+
+
+def _tone(gpu, oracle, lg, il, eid, ctx):
+    o = oracle.tone_lattice_decode(lg, il, eid)
+    g = gpu.tone_latent_lattice_beam_search_decode(_t(lg), _t(il), lg.shape[2], eid)
+    _same(g, o, TONE_OUT, ctx)
+
+
+@pytest.mark.parametrize("tie_rich", [False, True])
+def test_tone_config5(gpu, oracle, tie_rich):
+    """B=64 T=I=400 C=5 W=4 (20 candidates), ragged input lengths up to the step count."""
+    B, T, W, C = 64, 400, 4, 5
+    lg = oracle.synth_tone_logits(B, T, W, C, seed=20 + tie_rich, tie_rich=tie_rich)
+    il = np.random.default_rng(21).integers(T // 2, T + 1, size=B).astype(np.int32)
+    il[:8] = T
+    _tone(gpu, oracle, lg, il, 0, f"tie_rich={tie_rich}")
+
+
+def test_tone_more_candidates_than_lanes(gpu, oracle):
+    B, T, W, C = 4, 400, 16, 5
+    lg = oracle.synth_tone_logits(B, T, W, C, seed=22, tie_rich=True)
+    _tone(gpu, oracle, lg, np.full(B, 390, np.int32), 0, "W*C=80")
+
+
+@pytest.mark.parametrize("seed", range(150))
+def test_tone_fused_random(gpu, oracle, seed):
+    c = dc.fused_tone_case(seed)
+    _tone(gpu, oracle, c["logits"], c["input_length"], c["empty_tone_id"], f"seed={seed}")
+
+
+V2_STEP = ("prediction", "log_prob", "next_t", "next_u", "next_is_finished",
+           "next_total_duration", "beam_branch")
+
+
+@pytest.mark.parametrize("W,D", [(4, 16), (5, 16), (2, 32), (8, 16)])
+@pytest.mark.parametrize("seed", range(10))
+def test_v2_single_step_long(gpu, oracle, W, D, seed):
+    """One v2 step at I=400, O=2000 with W*D = 64 and > 64 candidates."""
+    c = dc.v2_case_long(seed, W, D)
+    ol = np.zeros_like(c["output_length"]) if c["test_mode"] else c["output_length"]
+    o, rc = oracle.v2_step(c["h"], c["hist"], c["fin"], c["total"], c["table"], c["t"], c["u"],
+                           c["input_length"], ol, c["zero_duration_id"], c["allow_skip"],
+                           c["test_mode"])
+    args = (_t(c["h"]), _t(c["hist"]), _t(c["fin"]), _t(c["total"]), _t(c["table"]), _t(c["t"]),
+            _t(c["u"]), _t(c["input_length"]), _t(c["output_length"]), W, D,
+            c["zero_duration_id"], c["allow_skip"], c["test_mode"])
+    if rc == 3:
+        with pytest.raises(gpu.SsntError):
+            gpu.ssnt_tts_v2_beam_search_decode(*args)
+        return
+    g = gpu.ssnt_tts_v2_beam_search_decode(*args)
+    for k, v in zip(V2_STEP, g):
+        assert np.array_equal(v.cpu().numpy(), o[k]), (seed, k)

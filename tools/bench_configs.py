@@ -23,7 +23,11 @@ import oracle as O  # noqa: E402
 import ssnt_tts_amd as S  # noqa: E402
 
 DEV = torch.device("cuda:0")
-THREADS = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+sys.path.insert(0, str(ROOT))
+from bench import host_cpu_info  # noqa: E402
+
+HOST = host_cpu_info()
+THREADS = HOST["usable"]  # every core this process may run on (affinity, cgroup quota)
 
 
 def gpu_time(fn, iters, rounds=5):

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
-# GPU-box round check: parity tests, one bench line, rocprof kernel stats + PMC traffic.
-# Usage (via gpurun): bash tools/gpu_check.sh <tag>
+# GPU-box round check: parity tests, one bench line, the other configs, rocprof kernel stats +
+# PMC traffic. Usage (via gpurun): bash tools/gpu_check.sh <tag>
 set -euo pipefail
 TAG=${1:-r1}
 cd "$(dirname "$0")/.."
@@ -10,4 +10,6 @@ timeout -k 10 420 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeou
 tail -3 gpurun_out/pytest_gpu_${TAG}.log
 timeout -k 10 300 python3 bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
 cat gpurun_out/bench_${TAG}.json
+timeout -k 10 300 python3 tools/bench_configs.py > gpurun_out/configs_${TAG}.jsonl 2> gpurun_out/configs_${TAG}.err
+cat gpurun_out/configs_${TAG}.jsonl
 bash tools/profile_gpu.sh "$TAG"
