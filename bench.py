@@ -5,8 +5,9 @@ Workload (BASELINE.json configs[1], and configs[3] at N=8): per GPU B=256 uttera
 T=200 steps x U=80 positions, f32 log_trans (B,T,U,2) = log_softmax over {emit, shift} of
 z ~ N(0, 1.5^2) (synthetic, generated on device, seed = rank). One step = one fused
 fwd-bwd launch through the C-ABI (ssnt_fwd_bwd_sum_device) writing loss (B), grad (B,T,U,2)
-and the shard's loss sum (formed in the same launch), plus, for N > 1, an RCCL all-reduce of
-that scalar over xGMI.
+and the shard's loss sum (formed in the same launch). The K timed steps are one HIP graph at
+every N; for N > 1 the K per-step loss sums are all-reduced by one RCCL call over xGMI inside
+the timed region (timed_region()).
 Weak scaling: per-GPU work is fixed. value = all ranks' lattice cells / max-over-ranks time.
 
 roofline: algorithmic HBM bytes of the fwd-bwd kernel = 16 B/cell (read 2xf32 log_trans, write
@@ -144,17 +145,16 @@ def main():
     out = {"loss": torch.empty(B, device=dev), "grad": torch.empty((B, T, U, 2), device=dev),
            "status": torch.zeros(1, dtype=torch.int32, device=dev),
            "loss_sum": torch.zeros(1, device=dev)}
-    total = out["loss_sum"]
 
     # correctness/status check once through the full Python mirror, outside the timed region
     r = S.ssnt_fwd_bwd(lt, sl, pl, out=out, check=True, loss_sum=True)
     assert torch.isfinite(r["loss"]).all()
     assert torch.isclose(r["loss_sum"], r["loss"].double().sum().float(), rtol=1e-5).all()
 
-    # The timed loop calls the C ABI directly (pointers bound once). N=1: the K steps are one
-    # HIP graph of K kernel launches, replayed with one call (the host issues nothing per step).
-    # N>1: eager launches; each step's loss sum is all-reduced by RCCL asynchronously into one of
-    # two alternating buffers, so the collective overlaps the next step's kernel.
+    # The timed loop calls the C ABI directly (pointers bound once). N=1 and N>1 run the same
+    # loop: the K steps are one HIP graph of K launches (the host issues nothing per step), each
+    # step writing its shard's loss sum into its own slot of `sums`; N>1 then all-reduces the K
+    # per-step sums with one RCCL call inside the timed region.
     import ctypes
     lib = S.load()
     wsb = int(lib.ssnt_fwd_bwd_workspace_size(B, T, U))
@@ -162,108 +162,100 @@ def main():
     sum_state = torch.zeros(int(lib.ssnt_fwd_bwd_sum_state_size(B)), dtype=torch.uint8, device=dev)
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
     vp = ctypes.c_void_p
-    totals = [total, torch.zeros(1, device=dev)]
+    K = args.steps
+    sums = torch.zeros(K, device=dev)
 
-    def cargs_for(stream, tot):
-        return (vp(lt.data_ptr()), None, vp(sl.data_ptr()), vp(pl.data_ptr()), B, T, U, 1,
-                vp(out["loss"].data_ptr()), vp(out["grad"].data_ptr()), None, None, None,
-                vp(ws.data_ptr()) if wsb else None, wsb, None, vp(tot.data_ptr()),
-                vp(sum_state.data_ptr()), vp(stream.cuda_stream))
-
-    def launch(cargs):
-        rc = lib.ssnt_fwd_bwd_sum_device(*cargs)
+    def launch(stream, k):
+        rc = lib.ssnt_fwd_bwd_sum_device(
+            vp(lt.data_ptr()), None, vp(sl.data_ptr()), vp(pl.data_ptr()), B, T, U, 1,
+            vp(out["loss"].data_ptr()), vp(out["grad"].data_ptr()), None, None, None,
+            vp(ws.data_ptr()) if wsb else None, wsb, None, vp(sums[k].data_ptr()),
+            vp(sum_state.data_ptr()), vp(stream.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"ssnt_fwd_bwd_sum_device: {S.status_string(rc)}")
 
-    main = torch.cuda.current_stream(dev)
-    K = args.steps
+    main_stream = torch.cuda.current_stream(dev)
+    for k in range(args.warmup):
+        launch(main_stream, k % K)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(dev)
+    with torch.cuda.graph(graph, stream=cap):
+        for k in range(K):
+            launch(cap, k)
+    graph.replay()  # first replay uploads the graph (untimed)
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if not dist:
-        a_main = cargs_for(main, total)
-        for _ in range(args.warmup):
-            launch(a_main)
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        cap = torch.cuda.Stream(dev)
-        with torch.cuda.graph(graph, stream=cap):
-            a_cap = cargs_for(cap, total)
-            for _ in range(K):
-                launch(a_cap)
-        graph.replay()  # first replay uploads the graph (untimed)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        e0.record(main)
+
+    def replay():
+        e0.record(main_stream)
         graph.replay()
-        e1.record(main)
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-    else:
-        a_alt = [cargs_for(main, t) for t in totals]
-        works = []
+        e1.record(main_stream)
 
-        def step(i):
-            if i >= 2:
-                works[i - 2].wait()  # stream-side: buffer i%2 is free again
-            launch(a_alt[i % 2])
-            works.append(torch.distributed.all_reduce(totals[i % 2], async_op=True))
-
-        for i in range(args.warmup):
-            step(i)
-        for w in works:
-            w.wait()
-        works.clear()
-        torch.cuda.synchronize()
-        torch.distributed.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        e0.record(main)
-        for i in range(K):
-            step(i)
-        for w in works:
-            w.wait()
-        e1.record(main)
-        torch.cuda.synchronize()
-        torch.distributed.barrier()
-        elapsed = time.perf_counter() - t0
-    # average kernel duration: the launch stream's events over the K back-to-back launches
+    reduce = (lambda x: torch.distributed.all_reduce(x)) if dist else None
+    elapsed = timed_region(replay, sums, reduce, torch.cuda.synchronize,
+                           torch.distributed.barrier if dist else None)
+    # average kernel duration: the launch stream's events around the K back-to-back launches
     kern_ms = e0.elapsed_time(e1) / K
     if dist:
         t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-
-    cells_step = world * B * T * U
-    value = cells_step * K / elapsed
-    achieved = B * T * U * BYTES_PER_CELL / (kern_ms * 1e-3) / 1e9  # GB/s per GPU
+        # every step's reduced sum is the global batch loss (one shard per rank)
+        assert torch.isfinite(sums).all()
     if rank == 0:
-        res = {
-            "metric": BASELINE["metric"],
-            "value": value,
-            "unit": "cells/s",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / K * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (log_softmax of N(0,1.5^2) logits, generated on device)",
-            "config": {"workload": f"lattice fwd-bwd loss+grad, B={B}/GPU T={T} U={U} "
-                                   "(BASELINE configs[1]; configs[3] at N=8)",
-                       "global_batch": world * B, "T": T, "U": U,
-                       "parallelism": f"batch-sharded x{world}, RCCL loss all-reduce" if dist
-                       else "single GPU"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": pmc_traffic(),
-                         "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": B * T * U * BYTES_PER_CELL},
-        }
+        res = result_line(world, B, T, U, K, args.warmup, elapsed, kern_ms, dist)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(B, T, U)
         print(json.dumps(res), flush=True)
     if dist:
         torch.distributed.destroy_process_group()
+
+
+def timed_region(replay, sums, reduce, sync, barrier):
+    """The timed region shared by every N: barrier + sync; replay() runs the K steps (one HIP
+    graph on the GPU); N>1 all-reduces the K per-step loss sums once; sync + barrier. Returns
+    the wall time in seconds (this rank's; the caller takes the max over ranks)."""
+    if barrier:
+        barrier()
+    sync()
+    t0 = time.perf_counter()
+    replay()
+    if reduce is not None:
+        reduce(sums)
+    sync()
+    if barrier:
+        barrier()
+    return time.perf_counter() - t0
+
+
+def result_line(world, B, T, U, K, warmup, elapsed, kern_ms, dist):
+    cells_step = world * B * T * U
+    value = cells_step * K / elapsed
+    achieved = B * T * U * BYTES_PER_CELL / (kern_ms * 1e-3) / 1e9  # GB/s per GPU
+    return {
+        "metric": BASELINE["metric"],
+        "value": value,
+        "unit": "cells/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": warmup,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (log_softmax of N(0,1.5^2) logits, generated on device)",
+        "config": {"workload": f"lattice fwd-bwd loss+grad, B={B}/GPU T={T} U={U} "
+                               "(BASELINE configs[1]; configs[3] at N=8)",
+                   "global_batch": world * B, "T": T, "U": U,
+                   "parallelism": (f"batch-sharded x{world}, one RCCL all-reduce of the K "
+                                   "per-step loss sums" if dist else "single GPU")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
+                     "traffic": pmc_traffic(),
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": B * T * U * BYTES_PER_CELL},
+    }
 
 
 if __name__ == "__main__":

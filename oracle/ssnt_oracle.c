@@ -68,14 +68,26 @@ static inline int32_t f2i_sat(float x) {
     return (int32_t)x;
 }
 
+/* Sort key: the IEEE order of `partial_cmp` (src/lib.rs:161) -- -0 and +0 share a key --
+ * extended to a total order with NaN below -inf (the GPU kernels use the same key). NaN keys are
+ * outside the parity contract: Rust's result for them depends on its sort implementation. */
+static inline uint32_t lp_key(float x) {
+    if (x != x) return 1u;
+    uint32_t bits;
+    if (x == 0.0f) bits = 0u;
+    else memcpy(&bits, &x, 4);
+    return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+}
+
 /* Stable sort by log_prob descending; `partial_cmp(..).unwrap_or(Equal).reverse()`
  * (src/lib.rs:161). Insertion sort = stable; element moves before its predecessor only when
- * strictly greater. NaN keys are outside the parity contract. */
+ * its key is strictly greater. */
 static void sort_desc_stable(cand_t *c, int n) {
     for (int i = 1; i < n; ++i) {
         cand_t x = c[i];
+        const uint32_t kx = lp_key(x.lp);
         int j = i - 1;
-        while (j >= 0 && c[j].lp < x.lp) {
+        while (j >= 0 && lp_key(c[j].lp) < kx) {
             c[j + 1] = c[j];
             --j;
         }

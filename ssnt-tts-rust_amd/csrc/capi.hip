@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "ssnt_internal.h"
@@ -67,7 +68,14 @@ int ctx_ready(const char* fn, bool abort_on_error) {
     return SSNT_ERR_HIP;
   }
   if (g_ctx.device != dev) {
-    // a different device for this thread: drop old resources (they belong to another device)
+    // a different device for this thread: release the old device's stream and buffers (HIP
+    // frees device allocations and streams from any current device)
+    if (g_ctx.stream) {
+      (void)hipStreamSynchronize(g_ctx.stream);
+      (void)hipStreamDestroy(g_ctx.stream);
+    }
+    if (g_ctx.d) (void)hipFree(g_ctx.d);
+    if (g_ctx.h) (void)hipHostFree(g_ctx.h);
     g_ctx = HostCtx{};
     g_ctx.device = dev;
     if (hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking) != hipSuccess) {
@@ -110,7 +118,16 @@ int ensure(size_t dbytes, size_t hbytes, const char* fn, bool abort_on_error) {
   return SSNT_OK;
 }
 
-// Staging plan: a list of host arrays laid out in one buffer (inputs first, then outputs).
+// Host staging mode for the small per-step reference symbols (not ssnt_fwd_bwd, whose tensors
+// are large): 0 = one H2D copy of inputs + zeroed status word, kernel, one D2H copy; 1 =
+// zero-copy: the kernel reads its inputs from and writes its outputs to the pinned staging
+// buffer over the bus (no copies; launch + synchronise only). Default measured per DESIGN.md
+// (tools/bench_step_symbols.py); atomic, so concurrent callers never race on it.
+std::atomic<int> g_host_mode{1};
+constexpr size_t kZeroCopyMax = 1 << 20;  // plans up to this size may run zero-copy
+
+// Staging plan: a list of host arrays laid out in one buffer: inputs, the status word, then the
+// outputs, so a single H2D copy covers the inputs and the zeroed status word.
 struct Slot {
   const void* src;  // host input (null for pure outputs)
   void* dst;        // host output (null for pure inputs)
@@ -120,7 +137,9 @@ struct Slot {
 
 struct Plan {
   std::vector<Slot> in, out;
-  size_t in_bytes = 0, total = 0;
+  size_t status_off = 0, total = 0;
+  bool zero_copy = false;
+  char* dbase = nullptr;  // what the kernel addresses: device scratch, or the mapped staging buffer
   static size_t align(size_t x) { return (x + 255) & ~size_t(255); }
   int add_in(const void* src, size_t bytes) {
     in.push_back(Slot{src, nullptr, bytes, 0});
@@ -133,35 +152,48 @@ struct Plan {
   void layout() {
     size_t o = 0;
     for (auto& s : in) { s.off = o; o += align(s.bytes); }
+    status_off = o;
+    o += 256;
     // outputs that need their previous contents (init) are uploaded too
     for (auto& s : out) { s.off = o; o += align(s.bytes); }
-    in_bytes = o;
-    total = o + 256;  // + status word
+    total = o;
   }
-  template <typename T> T* din(int i) const { return reinterpret_cast<T*>(g_ctx.d + in[i].off); }
-  template <typename T> T* dout(int i) const { return reinterpret_cast<T*>(g_ctx.d + out[i].off); }
-  int* dstatus() const { return reinterpret_cast<int*>(g_ctx.d + in_bytes); }
+  template <typename T> T* din(int i) const { return reinterpret_cast<T*>(dbase + in[i].off); }
+  template <typename T> T* dout(int i) const { return reinterpret_cast<T*>(dbase + out[i].off); }
+  int* dstatus() const { return reinterpret_cast<int*>(dbase + status_off); }
 };
 
-// Upload inputs (and output init contents), zero the status word.
-int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device = 0) {
+// Stage inputs (and output init contents) and a zeroed status word: one H2D copy, or none in
+// zero-copy mode. `allow_zero_copy`: the per-step symbols only.
+int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device = 0,
+             bool allow_zero_copy = true) {
   p.layout();
-  int rc = ensure(Plan::align(p.total) + extra_device, p.total, fn, abort_on_error);
+  p.zero_copy = allow_zero_copy && extra_device == 0 && p.total <= kZeroCopyMax &&
+                g_host_mode.load(std::memory_order_relaxed) == 1;
+  int rc = ensure(p.zero_copy ? 0 : Plan::align(p.total) + extra_device, p.total, fn,
+                  abort_on_error);
   if (rc != SSNT_OK) return rc;
+  if (p.zero_copy) {
+    void* mapped = nullptr;
+    if (hipHostGetDevicePointer(&mapped, g_ctx.h, 0) != hipSuccess || mapped == nullptr) {
+      p.zero_copy = false;  // not mappable here: fall back to the copies
+      rc = ensure(Plan::align(p.total) + extra_device, p.total, fn, abort_on_error);
+      if (rc != SSNT_OK) return rc;
+    } else {
+      p.dbase = static_cast<char*>(mapped);
+    }
+  }
+  if (!p.zero_copy) p.dbase = g_ctx.d;
   for (auto& s : p.in) memcpy(g_ctx.h + s.off, s.src, s.bytes);
-  size_t up_end = 0;
-  for (auto& s : p.in) up_end = s.off + s.bytes;
+  memset(g_ctx.h + p.status_off, 0, sizeof(int));
+  size_t up_end = p.status_off + sizeof(int);
   for (auto& s : p.out)
     if (s.src) {
       memcpy(g_ctx.h + s.off, s.src, s.bytes);
       up_end = s.off + s.bytes;
     }
-  memset(g_ctx.h + p.in_bytes, 0, sizeof(int));
-  hipError_t e = hipSuccess;
-  if (up_end) e = hipMemcpyAsync(g_ctx.d, g_ctx.h, up_end, hipMemcpyHostToDevice, g_ctx.stream);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(g_ctx.d + p.in_bytes, g_ctx.h + p.in_bytes, sizeof(int),
-                       hipMemcpyHostToDevice, g_ctx.stream);
+  if (p.zero_copy) return SSNT_OK;
+  const hipError_t e = hipMemcpyAsync(g_ctx.d, g_ctx.h, up_end, hipMemcpyHostToDevice, g_ctx.stream);
   if (e != hipSuccess) {
     if (abort_on_error) fail(fn, hipGetErrorString(e));
     return SSNT_ERR_HIP;
@@ -169,25 +201,25 @@ int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device =
   return SSNT_OK;
 }
 
-// Download outputs + status, synchronise, scatter to the caller's arrays. Returns status code.
+// Download status + outputs (one D2H copy, none in zero-copy mode), synchronise, scatter to the
+// caller's arrays. Returns status code.
 int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
   if (launch_rc != SSNT_OK) {
     if (abort_on_error) fail(fn, ssnt_status_string(launch_rc));
     return launch_rc;
   }
-  size_t lo = p.in_bytes, hi = p.in_bytes + sizeof(int);
-  for (auto& s : p.out) {
-    lo = std::min(lo, s.off);
-    hi = std::max(hi, s.off + s.bytes);
+  hipError_t e = hipSuccess;
+  if (!p.zero_copy) {
+    const size_t lo = p.status_off, hi = p.total;
+    e = hipMemcpyAsync(g_ctx.h + lo, g_ctx.d + lo, hi - lo, hipMemcpyDeviceToHost, g_ctx.stream);
   }
-  hipError_t e = hipMemcpyAsync(g_ctx.h + lo, g_ctx.d + lo, hi - lo, hipMemcpyDeviceToHost, g_ctx.stream);
   if (e == hipSuccess) e = hipStreamSynchronize(g_ctx.stream);
   if (e != hipSuccess) {
     if (abort_on_error) fail(fn, hipGetErrorString(e));
     return SSNT_ERR_HIP;
   }
   int bits = 0;
-  memcpy(&bits, g_ctx.h + p.in_bytes, sizeof(int));
+  memcpy(&bits, g_ctx.h + p.status_off, sizeof(int));
   const int rc = status_bits_to_code(bits);
   if (rc != SSNT_OK) {
     if (abort_on_error) {
@@ -456,6 +488,13 @@ void tone_latent_levenshtein_edit_distance(const int* a, const int* b, const int
 
 int ssnt_fwd_bwd_set_variant(int variant) { return set_fwd_bwd_variant(variant); }
 
+// A/B of the host staging of the per-step reference symbols (tools/bench_step_symbols.py);
+// not part of the public header. 0 = copies, 1 = zero-copy. Returns the previous mode.
+int ssnt_set_host_staging(int mode) {
+  if (mode != 0 && mode != 1) return -1;
+  return g_host_mode.exchange(mode);
+}
+
 // diagnostic builds (make lib-diag) only; not part of the public header
 int ssnt_diag_read(void* host, size_t bytes) { return diag_read(host, bytes); }
 
@@ -519,7 +558,7 @@ int ssnt_fwd_bwd(const float* log_trans, const float* log_obs, const int* step_l
   const int ogo = grad_obs ? p.add_out(grad_obs, cells * 4) : -1;
   const int ola = log_alpha ? p.add_out(log_alpha, cells * 4) : -1;
   const int olb = log_beta ? p.add_out(log_beta, cells * 4) : -1;
-  rc = stage_in(p, fn, false, ws);  // the workspace is device-only, reserved after the plan
+  rc = stage_in(p, fn, false, ws, false);  // device-only workspace reserved after the plan
   if (rc != SSNT_OK) return rc;
   const size_t ws_off = Plan::align(p.total);
   FwdBwdArgs a{};
@@ -621,22 +660,6 @@ int ssnt_lattice_beam_search_decode_device(const float* lattice, const int* inpu
   a.next_fin = next_is_finished; a.beam_branch = beam_branch;
   a.best_beam_branch = best_beam_branch; a.best_t_history = best_t_history; a.status = status;
   return launch_fused_decode(a, as_stream(stream));
-}
-
-// round-2 A/B only (not in the public header): the round-1 fused v1 kernel + k_backtrace
-int ssnt_lattice_decode_r1_device(const float* lattice, const int* input_length, int batch_size,
-                                  int max_steps, int max_pos, int beam_width, int* prediction,
-                                  float* log_probs, int* next_t, int* next_u,
-                                  bool* next_is_finished, int* beam_branch,
-                                  int* best_beam_branch, int* best_t_history, int* status,
-                                  void* stream) {
-  LatticeDecodeArgs a{};
-  a.B = batch_size; a.T = max_steps; a.U = max_pos; a.W = beam_width;
-  a.lattice = lattice; a.input_length = input_length;
-  a.prediction = prediction; a.log_prob = log_probs; a.next_t = next_t; a.next_u = next_u;
-  a.next_fin = next_is_finished; a.beam_branch = beam_branch;
-  a.best_beam_branch = best_beam_branch; a.best_t_history = best_t_history; a.status = status;
-  return launch_lattice_decode(a, as_stream(stream));
 }
 
 int ssnt_v2_lattice_beam_search_decode_device(

@@ -28,6 +28,16 @@ __device__ __forceinline__ int f2i_sat(float x) {
   return (int)x;
 }
 
+// Sort key of a log-prob: the IEEE order of the reference's comparison (src/lib.rs:161), so -0
+// and +0 share a key, extended to a total order by placing NaN below -inf. NaN inputs are
+// outside the parity contract; the total order only guarantees that ranks are
+// a permutation (every output stays in range). Never 0: 0 marks "no candidate".
+__device__ __forceinline__ unsigned lp_key(float x) {
+  if (x != x) return 1u;
+  const unsigned bits = x == 0.0f ? 0u : __float_as_uint(x);
+  return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+}
+
 __device__ __forceinline__ bool cand_eq(const Cand& a, const Cand& b, bool with_tot) {
   return a.pred == b.pred && a.lp == b.lp && a.nt == b.nt && a.nu == b.nu && a.fin == b.fin &&
          (!with_tot || a.tot == b.tot);
@@ -145,11 +155,12 @@ __device__ int step_wave(const StepArgs& a, const BatchView& v, Cand* cand, int*
     const Cand me = cand[c];
     if (!me.valid) continue;
     ++nvalid_local;
+    const unsigned km = lp_key(me.lp);
     int rank = 0;
     for (int j = 0; j < n; ++j) {
-      const float lj = cand[j].lp;
+      const unsigned kj = lp_key(cand[j].lp);
       const int vj = cand[j].valid;
-      rank += (vj && (lj > me.lp || (lj == me.lp && j < c))) ? 1 : 0;
+      rank += (vj && (kj > km || (kj == km && j < c))) ? 1 : 0;
     }
     order[rank] = c;
   }

@@ -7,7 +7,7 @@
 //
 //   n <= 64  k_fused_reg: one candidate per lane; only the sort keys and the staged outputs touch
 //            LDS.
-//     rank     #{j : key_j > key_c} with key = (sortable(lp), 63 - c): the stable descending sort
+//     rank     #{j : key_j > key_c} with key = (lp_key(lp), 63 - c): the stable descending sort
 //              of src/lib.rs:161 (ties keep generation order), over broadcast LDS reads
 //     sort     ds_permute of the packed candidate fields to lane = rank
 //     dedup    compare with the DPP-shifted left neighbour (src/lib.rs:162, eq_ignore_parent)
@@ -33,13 +33,6 @@ constexpr int kV1Regs = 4;   // v1 lattice row floats per lane: the row is stage
 constexpr int kChunk = 32;   // per-step outputs staged in LDS and flushed every kChunk steps
 constexpr int kRing = 7;     // staged output arrays
 
-// IEEE total order of the reference's comparison (src/lib.rs:161): -0 and +0 compare equal, so
-// both map to one key. NaN is outside the parity contract.
-__device__ __forceinline__ unsigned sortable(float x) {
-  const unsigned bits = x == 0.0f ? 0u : __float_as_uint(x);
-  return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
-}
-
 // One wave per workgroup: LDS operations of a wave complete in order, so a write followed by a
 // read of the same location needs no barrier -- only the compiler must keep the order.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
@@ -56,7 +49,9 @@ struct RegLayout {
   }
 };
 
-template <Variant V, bool STAGED>
+// NMAX: a compile-time bound on n (8, 16, 32 or 64): the rank loop is unrolled to NMAX so its
+// broadcast key reads are issued back to back instead of one LDS round trip per pair.
+template <Variant V, bool STAGED, int NMAX>
 __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kV1 = V == Variant::V1, kV2 = V == Variant::V2;
@@ -184,12 +179,13 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     if constexpr (!kV1) load_row(s + kAhead, row);
     valid = valid && is_cand;
     // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
-    const u64 key = ((u64)(valid ? sortable(lp) : 0u) << 32) | (unsigned)(63 - lane);
+    const u64 key = ((u64)(valid ? lp_key(lp) : 0u) << 32) | (unsigned)(63 - lane);
     keys[lane] = key;
     lds_order();
     int rank = 0;
-    const int n2 = (n + 1) & ~1;
-    for (int j = 0; j < n2; j += 2) {
+    // keys of lanes >= n are below every valid key (their high word is 0): reading them is harmless
+#pragma unroll
+    for (int j = 0; j < NMAX; j += 2) {
       const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(keys + j);  // broadcast read
       rank += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
     }
@@ -427,15 +423,24 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
   const int n = a.W * C;
   const bool want_paths = a.ordered || a.path_pred || a.duration || a.best_beam_branch;
   bool paths_kernel = want_paths;
-  int rc;
+  int rc = SSNT_OK;
   if (n <= 64) {
     const bool staged = V != Variant::V1 || 2 * (size_t)a.U <= 64 * (size_t)kV1Regs;
     const bool hist_lds = RegLayout(V, a.W, a.T, a.U, true, staged).total <= kMaxLds;
     const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged).total;
     if (lds > kMaxLds) return SSNT_ERR_UNSUPPORTED;
-    if (staged) rc = launch_with_lds(k_fused_reg<V, true>, lds, a.B, st, a, hist_lds ? 1 : 0);
-    else if constexpr (V == Variant::V1)  // only v1 rows can be too long to stage
-      rc = launch_with_lds(k_fused_reg<V, false>, lds, a.B, st, a, hist_lds ? 1 : 0);
+    const int h = hist_lds ? 1 : 0;
+    if (!staged) {  // only v1 rows can be too long to stage
+      if constexpr (V == Variant::V1) rc = launch_with_lds(k_fused_reg<V, false, 64>, lds, a.B, st, a, h);
+    } else if (n <= 8) {
+      rc = launch_with_lds(k_fused_reg<V, true, 8>, lds, a.B, st, a, h);
+    } else if (n <= 16) {
+      rc = launch_with_lds(k_fused_reg<V, true, 16>, lds, a.B, st, a, h);
+    } else if (n <= 32) {
+      rc = launch_with_lds(k_fused_reg<V, true, 32>, lds, a.B, st, a, h);
+    } else {
+      rc = launch_with_lds(k_fused_reg<V, true, 64>, lds, a.B, st, a, h);
+    }
     paths_kernel = want_paths && !hist_lds;
   } else {
     const size_t lds = (size_t)n * sizeof(Cand) + 2 * (size_t)n * 4 + (size_t)a.W * 2 * 16 +

@@ -21,6 +21,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <mutex>
+
 #include "lattice_dev.h"
 
 namespace ssnt {
@@ -284,14 +287,11 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 template <int K, bool OBS, bool LDS, bool VEC>
 int launch_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
   auto kern = k_fwd_bwd<K, OBS, LDS, VEC>;
-  if (lds > 64 * 1024) {  // dynamic LDS above 64 KiB needs the attribute (idempotent)
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
-      attr_set = true;
-    }
-  }
+  // dynamic LDS above 64 KiB needs the attribute; it is per device, so it is set on every such
+  // launch (a host-side call, no device work) rather than cached in a process-wide flag
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
   hipLaunchKernelGGL(kern, dim3(a.B), dim3(128), lds, st, a);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
@@ -321,10 +321,18 @@ int launch_simple(const FwdBwdArgs& a, hipStream_t st) {
   return SSNT_ERR_UNSUPPORTED;
 }
 
-// -1: not chosen yet (env SSNT_FWD_BWD_KERNEL=simple selects 1), 0 streaming kernel
-// (fwd_bwd_stream.hip; falls back to the two-wave kernel for shapes it does not take),
-// 1 two-wave kernel only
-int g_variant = -1;
+// 0 streaming kernel (fwd_bwd_stream.hip; falls back to the two-wave kernel for shapes it does
+// not take), 1 two-wave kernel only. Process-wide A/B switch: read from the environment once
+// (SSNT_FWD_BWD_KERNEL=simple selects 1), atomic so concurrent callers never race on it.
+std::atomic<int> g_variant{0};
+std::once_flag g_variant_env;
+int variant() {
+  std::call_once(g_variant_env, [] {
+    const char* e = getenv("SSNT_FWD_BWD_KERNEL");
+    if (e && strcmp(e, "simple") == 0) g_variant.store(1);
+  });
+  return g_variant.load(std::memory_order_relaxed);
+}
 
 }  // namespace
 
@@ -340,9 +348,14 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
 }
 
 int set_fwd_bwd_variant(int v) {
-  // 0 stream, 1 two-wave; 2..10: stream with another wave mix / ring / publication (tuning only)
+  // 0 stream, 1 two-wave; 2..10 (SSNT_EXP builds only): stream with another wave mix / ring /
+  // publication period (tuning)
   if (v < 0 || v > 10) return SSNT_ERR_INVALID_ARG;
-  g_variant = v >= 2 ? 0 : v;
+#ifndef SSNT_EXP
+  if (v >= 2) return SSNT_ERR_UNSUPPORTED;
+#endif
+  variant();  // the environment is read once, before any explicit choice
+  g_variant.store(v >= 2 ? 0 : v);
   set_stream_mix(v >= 2 ? v - 1 : 0);
   return SSNT_OK;
 }
@@ -355,11 +368,7 @@ __global__ __launch_bounds__(64) void k_loss_sum(const float* loss, int B, float
 
 int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
   summed = false;
-  if (g_variant < 0) {
-    const char* e = getenv("SSNT_FWD_BWD_KERNEL");
-    g_variant = (e && strcmp(e, "simple") == 0) ? 1 : 0;
-  }
-  if (g_variant == 0) {
+  if (variant() == 0) {
     FwdBwdArgs x = a;
 #ifdef SSNT_EXP
     const char* ee = getenv("SSNT_EXP");

@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
+#include <atomic>
 #include <type_traits>
 #include <utility>
 
@@ -924,14 +925,11 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 template <int K, bool OBS, bool LDS, int NC, int NH, int RS>
 int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
   auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH, RS>;
-  if (lds > 64 * 1024) {  // dynamic LDS above 64 KiB needs the attribute (idempotent)
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
-      attr_set = true;
-    }
-  }
+  // dynamic LDS above 64 KiB needs the attribute; it is per device, so it is set on every such
+  // launch (a host-side call, no device work) rather than cached in a process-wide flag
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
   hipLaunchKernelGGL(kern, dim3(a.B), dim3(64 * (2 + 2 * NC + 2 * NH)), lds, st, a);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
@@ -994,12 +992,16 @@ size_t stream_head_bytes(int K, int U, bool obs, int ring) {
          2 * (size_t)R2 * U * sizeof(xf);
 }
 
-int g_mix = 0;  // tuning knob (ssnt_fwd_bwd_set_variant >= 2)
+#ifdef SSNT_EXP
+std::atomic<int> g_mix{0};  // tuning knob (ssnt_fwd_bwd_set_variant >= 2; SSNT_EXP builds only)
+#endif
 
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
+#ifdef SSNT_EXP
   // tuning mixes (ssnt_fwd_bwd_set_variant >= 2): K = 2 without log_obs only, else the default
-  if (g_mix != 0 && !a.log_obs && a.U > 64 && a.U <= 128) {
-    switch (g_mix) {
+  const int mix = g_mix.load(std::memory_order_relaxed);
+  if (mix != 0 && !a.log_obs && a.U > 64 && a.U <= 128) {
+    switch (mix) {
       case 1: return launch_stream_k<2, false, 4, 2>(a, st);
       case 2: return launch_stream_k<2, false, 3, 2>(a, st);
       case 3: return launch_stream_k<2, false, 2, 4>(a, st);
@@ -1012,9 +1014,16 @@ int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
       default: break;
     }
   }
+#endif
   return a.log_obs ? launch_stream_obs<true>(a, st) : launch_stream_obs<false>(a, st);
 }
 
-void set_stream_mix(int m) { g_mix = m; }
+void set_stream_mix(int m) {
+#ifdef SSNT_EXP
+  g_mix.store(m);
+#else
+  (void)m;
+#endif
+}
 
 }  // namespace ssnt

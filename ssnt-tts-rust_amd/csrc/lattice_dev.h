@@ -407,8 +407,15 @@ __device__ __forceinline__ void finish_loss_sum(const FwdBwdArgs& a, unsigned ta
     for (int i = lane; i < a.B; i += 64)
       ok &= (unsigned)(__hip_atomic_load(sum_granule(a, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag;
     if (__all(ok)) break;
-    if (spins > (1 << 24)) {  // bounded (~4 s): report and give up (the sum is then not written)
-      if (lane == 0 && a.status) atomicOr(a.status, kStatusTimeout);
+    if (spins > (1 << 24)) {  // bounded (~4 s): report, poison the sum, still advance the epoch
+      // (a later launch must never accept this launch's granules: its tag is epoch + 1 again
+      // only if the epoch moved on)
+      if (lane == 0) {
+        if (a.status) atomicOr(a.status, kStatusTimeout);
+        *a.loss_sum = __builtin_nanf("");
+        __hip_atomic_store(reinterpret_cast<unsigned*>(a.sum_state), tag, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
       return;
     }
     __builtin_amdgcn_s_sleep(8);

@@ -76,22 +76,6 @@ struct StepArgs {
 };
 int launch_decode_step(const StepArgs& a, hipStream_t stream);
 
-struct LatticeDecodeArgs {
-  int B, T, U, W;
-  const float* lattice;      // (B,T,U,2)
-  const int* input_length;   // (B)
-  int* prediction;           // (B,T,W)
-  float* log_prob;           // (B,T,W)
-  int* next_t;               // (B,T,W)
-  int* next_u;               // (B,T,W)
-  bool* next_fin;            // (B,T,W)
-  int* beam_branch;          // (B,T,W)
-  int* best_beam_branch;     // (B,T)
-  int* best_t_history;       // (B,T)
-  int* status;
-};
-int launch_lattice_decode(const LatticeDecodeArgs& a, hipStream_t stream);
-
 // Fused multi-step decode (fused_decode.hip): all beams start at t = u = 0, log-prob 0,
 // total 0, not finished; step s feeds the exact per-step contract with
 //   V1:        h[w] = src[b, s, t_w, :]  (src = (B,T,U,2) lattice; live beams have u_w == s)

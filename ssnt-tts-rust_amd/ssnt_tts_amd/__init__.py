@@ -243,18 +243,13 @@ def levenshtein_edit_distance(a, b, a_lengths, b_lengths, *, check=True):
 # ----------------------------------------------------------------------------------------------
 # Lattice forward-backward (DESIGN.md "Lattice semantics")
 # ----------------------------------------------------------------------------------------------
-_ws_cache: dict = {}
-
-
 def _workspace(dev, nbytes):
+    """Row workspace for one call, from torch's caching allocator on the current stream: reuse
+    is free after the first call, and a buffer is never shared by launches on different streams
+    (the allocator tracks the stream each block was allocated on)."""
     if nbytes == 0:
         return None
-    key = (dev.index if dev.index is not None else torch.cuda.current_device())
-    buf = _ws_cache.get(key)
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        _ws_cache[key] = buf
-    return buf
+    return torch.empty(nbytes, dtype=torch.uint8, device=dev)
 
 
 _sum_states = {}
@@ -342,31 +337,36 @@ def ssnt_fwd_bwd(log_trans, step_len, pos_len, log_obs=None, *, terminal_emit=Tr
 
 
 class SSNTLatticeLoss(torch.autograd.Function):
-    """Autograd wrapper: per-utterance loss (B,), gradients computed in the same kernel launch."""
+    """Autograd wrapper: per-utterance loss (B,), gradients computed in the same kernel launch.
+    The launch's status word (bad lengths, a bounded intra-kernel wait that expired) is checked
+    in backward, where the step synchronises anyway (check=False skips it)."""
 
     @staticmethod
     def forward(ctx, log_trans, step_len, pos_len, log_obs=None, terminal_emit=True,
-                zero_infinity=False):
+                zero_infinity=False, check=True):
         need = log_trans.requires_grad or (log_obs is not None and log_obs.requires_grad)
         r = ssnt_fwd_bwd(log_trans.detach(), step_len, pos_len,
                          None if log_obs is None else log_obs.detach(),
                          terminal_emit=terminal_emit, zero_infinity=zero_infinity, need_grad=need)
-        ctx.save_for_backward(r.get("grad"), r.get("grad_obs"))
+        ctx.save_for_backward(r.get("grad"), r.get("grad_obs"), r["status"])
+        ctx.check = check
         return r["loss"]
 
     @staticmethod
     def backward(ctx, grad_loss):
-        g, go = ctx.saved_tensors
+        g, go, st = ctx.saved_tensors
+        if ctx.check:
+            _finish("ssnt_lattice_loss", 0, st, True)
         gl = grad_loss.to(torch.float32)
         gt = None if g is None else g * gl[:, None, None, None]
         gobs = None if go is None else go * gl[:, None, None]
-        return gt, None, None, gobs, None, None
+        return gt, None, None, gobs, None, None, None
 
 
 def ssnt_lattice_loss(log_trans, step_len, pos_len, log_obs=None, terminal_emit=True,
-                      zero_infinity=False):
+                      zero_infinity=False, check=True):
     return SSNTLatticeLoss.apply(log_trans, step_len, pos_len, log_obs, terminal_emit,
-                                 zero_infinity)
+                                 zero_infinity, check)
 
 
 def lattice_beam_search_decode(lattice, input_length, beam_width, *, check=True):

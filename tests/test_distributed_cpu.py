@@ -72,3 +72,54 @@ def test_gloo_world2_loss_allreduce():
     for rank, total, lo, hi, grad in outs:
         assert abs(total - want) <= 1e-5 * max(1.0, abs(want))
         assert np.array_equal(grad, full["grad"][lo:hi])  # gradients stay local, unchanged
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's multi-rank step logic (timed_region + result_line) with gloo; each rank's
+    'replay' runs K steps of the C oracle on its shard and writes the per-step loss sums."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(root), str(root / "ssnt-tts-rust_amd"), str(root / "oracle")]
+    import bench
+    import oracle as O
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    Bg, T, U, K = 8, 20, 6, 3
+    lo, hi = shard_bounds(Bg, world, rank)
+    lt = O.synth_log_trans(Bg, T, U, seed=11)[lo:hi]
+    sums = torch.zeros(K)
+
+    def replay():
+        for k in range(K):
+            sums[k] = float(O.fwd_bwd_xf(lt, [T] * (hi - lo), [U] * (hi - lo))["loss"].sum())
+
+    elapsed = bench.timed_region(replay, sums, lambda x: torch.distributed.all_reduce(x),
+                                 lambda: None, torch.distributed.barrier)
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    line = bench.result_line(world, hi - lo, T, U, K, 0, float(t[0]), 0.01, True)
+    q.put((rank, sums.numpy().copy(), line, float(t[0])))
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world2_bench_step_logic():
+    import oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = O.fwd_bwd_xf(O.synth_log_trans(8, 20, 6, seed=11), [20] * 8, [6] * 8)["loss"]
+    want = float(np.sum(full, dtype=np.float64))
+    for rank, sums, line, elapsed in outs:
+        assert np.allclose(sums, want, rtol=1e-5)  # every step: the global batch loss
+        assert line["n_gpus"] == world and line["scaling"] == "weak"
+        assert line["config"]["global_batch"] == 8
+        assert abs(line["value"] - world * 4 * 20 * 6 * 3 / elapsed) < 1e-6 * line["value"]

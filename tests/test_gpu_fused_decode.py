@@ -164,3 +164,64 @@ def test_v2_single_step_long(gpu, oracle, W, D, seed):
     g = gpu.ssnt_tts_v2_beam_search_decode(*args)
     for k, v in zip(V2_STEP, g):
         assert np.array_equal(v.cpu().numpy(), o[k]), (seed, k)
+
+
+@pytest.mark.parametrize("kind", ["step_v1", "step_v2", "fused_v1", "fused_v2", "fused_tone"])
+def test_nan_inputs_stay_in_range(gpu, oracle, kind):
+    """NaN log-probs are outside the parity contract, but the rank must stay a
+    permutation: every output index in range, and the same total order (NaN below -inf) as the
+    oracle, so the outputs still match it."""
+    rng = np.random.default_rng(0)
+    if kind == "step_v1":
+        c = dc.v1_case(3, B=4, W=6, max_t=5)
+        c["h"][:, ::2, 0] = np.nan
+        c["hist"][:, 1] = np.nan
+        o = oracle.v1_step(c["h"], c["hist"], c["fin"], c["t"], c["u"], c["input_length"])
+        g = gpu.beam_search_decode(_t(c["h"]), _t(c["hist"]), _t(c["fin"]), _t(c["t"]), _t(c["u"]),
+                                   _t(c["input_length"]), 6)
+        bb = g[5].cpu().numpy()
+        assert ((bb >= 0) & (bb < 6)).all()
+        assert np.array_equal(bb, o["beam_branch"])
+        return
+    if kind == "step_v2":
+        c = dc.v2_case_long(1, 4, 16)
+        c["h"][:, :, 3:7] = np.nan
+        ol = np.zeros_like(c["output_length"]) if c["test_mode"] else c["output_length"]
+        o, rc = oracle.v2_step(c["h"], c["hist"], c["fin"], c["total"], c["table"], c["t"], c["u"],
+                               c["input_length"], ol, c["zero_duration_id"], c["allow_skip"],
+                               c["test_mode"])
+        g = gpu.ssnt_tts_v2_beam_search_decode(
+            _t(c["h"]), _t(c["hist"]), _t(c["fin"]), _t(c["total"]), _t(c["table"]), _t(c["t"]),
+            _t(c["u"]), _t(c["input_length"]), _t(c["output_length"]), 4, 16,
+            c["zero_duration_id"], c["allow_skip"], c["test_mode"], check=False)
+        bb = g[6].cpu().numpy()
+        assert ((bb >= 0) & (bb < 4)).all()
+        if rc == 0:
+            assert np.array_equal(bb, o["beam_branch"])
+        return
+    if kind == "fused_v1":
+        lat = oracle.synth_log_trans(8, 40, 16, seed=1)
+        lat[:, 5:9, 3:6, :] = np.nan
+        il = np.full(8, 16, np.int32)
+        o = oracle.v1_lattice_decode(lat, il, 4)
+        g = gpu.lattice_beam_search_decode(_t(lat), _t(il), 4)
+        for k in ("beam_branch", "best_beam_branch"):
+            v = g[k].cpu().numpy()
+            assert ((v >= 0) & (v < 4)).all()
+            assert np.array_equal(v, o[k]), k
+        return
+    if kind == "fused_v2":
+        lg, il, ol, _ = _config5(oracle, 3, B=8)
+        lg[:, 50:60, :, ::3] = np.nan
+        o, rc = oracle.v2_lattice_decode(lg, np.arange(16), il, ol, 0, False, True)
+        g = gpu.v2_lattice_beam_search_decode(_t(lg), _t(np.arange(16, dtype=np.int32)), _t(il),
+                                              _t(ol), 4, 0, False, True)
+        assert rc == 0
+        _same(g, o, ("beam_branch", "ordered_beam_branch", "prediction"), "nan v2")
+        return
+    lg = oracle.synth_tone_logits(8, 50, 4, 5, seed=4)
+    lg[:, 10:20, 1] = np.nan
+    il = np.full(8, 50, np.int32)
+    o = oracle.tone_lattice_decode(lg, il, 0)
+    g = gpu.tone_latent_lattice_beam_search_decode(_t(lg), _t(il), 4, 0)
+    _same(g, o, ("beam_branch", "ordered_beam_branch", "prediction"), "nan tone")

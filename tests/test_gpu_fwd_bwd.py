@@ -159,7 +159,10 @@ def test_tuning_wave_mixes_bit_exact(gpu, oracle, kernel_variant, variant):
     if kernel_variant != 0:
         pytest.skip("mix variants are streaming-kernel variants")
     lib = gpu.load()
-    assert lib.ssnt_fwd_bwd_set_variant(variant) == 0
+    rc = lib.ssnt_fwd_bwd_set_variant(variant)
+    if rc == 5:  # SSNT_ERR_UNSUPPORTED: the tuning mixes exist in `make lib-exp` builds only
+        pytest.skip("tuning mixes are compiled out of the product library")
+    assert rc == 0
     rng = np.random.default_rng(variant)
     B, T, U = 6, 90, 80
     P = rng.integers(1, U + 1, size=B)

@@ -4,7 +4,8 @@ with the CPU oracle timed beside each (a bounded sample). One JSON line per conf
 
   configs[0]  single utterance T=50 U=20 fwd-bwd (the reference's CPU-sized case)
   configs[2]  fused v1 beam-search decode B=256 T=200 U=80 W=4 (+ best-beam backtrace)
-  configs[4]  long form fwd-bwd B=64 T=2000 U=400 (K=8 layout, rows in the global workspace)
+  configs[4]  long form fwd-bwd B=64 T=2000 U=400; fused v2 decode B=64 I=400 O=2000 D=16 W=4
+              and fused tone decode B=64 I=400 C=5 W=4 (+ every final slot's path)
 GPU time: HIP events around `iters` back-to-back calls, median of 5 rounds (steady state).
 """
 import json
@@ -89,7 +90,44 @@ def decode_config(B, T, U, W, iters):
             "note": "latency-bound integer/compare work: HBM fraction << 1% (6.6 MB per launch)"}
 
 
+def v2_decode_config(B, I, Ototal, D, W, iters):
+    """configs[4] v2 path: fused decode of I=400 steps over per-step logits peaked on a sampled
+    duration path summing to O=2000, then every final slot's path + durations."""
+    d = O.synth_durations(B, I, Ototal, D, seed=0)
+    lg_np = O.synth_v2_logits(d, W, D, seed=100)
+    table_np = np.arange(D, dtype=np.int32)
+    il_np, ol_np = np.full(B, I, np.int32), np.full(B, Ototal, np.int32)
+    lg, table = torch.from_numpy(lg_np).to(DEV), torch.from_numpy(table_np).to(DEV)
+    il, ol = torch.from_numpy(il_np).to(DEV), torch.from_numpy(ol_np).to(DEV)
+    S.v2_lattice_beam_search_decode(lg, table, il, ol, W, 0, False, False)  # checks status
+    t = gpu_time(lambda: S.v2_lattice_beam_search_decode(lg, table, il, ol, W, 0, False, False,
+                                                         check=False), iters)
+    tc = cpu_time(lambda: O.v2_lattice_decode(lg_np, table_np, il_np, ol_np, 0, False, False,
+                                              n_threads=THREADS))
+    steps = B * I * W
+    return {"config": "configs[4] v2", "workload": f"fused v2 decode B={B} I={I} O={Ototal} "
+            f"D={D} W={W} + paths/durations", "gpu_us": t * 1e6, "beam_steps_per_s": steps / t,
+            "cpu_beam_steps_per_s": steps / tc, "cpu_threads": THREADS,
+            "note": f"{B} waves (one per utterance), {I} dependent steps of {W * D} candidates"}
+
+
+def tone_decode_config(B, I, C, W, iters):
+    lg_np = O.synth_tone_logits(B, I, W, C, seed=0)
+    il_np = np.full(B, I, np.int32)
+    lg, il = torch.from_numpy(lg_np).to(DEV), torch.from_numpy(il_np).to(DEV)
+    S.tone_latent_lattice_beam_search_decode(lg, il, W, 0)
+    t = gpu_time(lambda: S.tone_latent_lattice_beam_search_decode(lg, il, W, 0, check=False), iters)
+    tc = cpu_time(lambda: O.tone_lattice_decode(lg_np, il_np, 0, n_threads=THREADS))
+    steps = B * I * W
+    return {"config": "configs[4] tone", "workload": f"fused tone decode B={B} I={I} C={C} W={W} "
+            "+ paths", "gpu_us": t * 1e6, "beam_steps_per_s": steps / t,
+            "cpu_beam_steps_per_s": steps / tc, "cpu_threads": THREADS}
+
+
 if __name__ == "__main__":
     print(json.dumps(fwd_bwd_config("configs[0]", 1, 50, 20, iters=50, cpu_sample=1)), flush=True)
     print(json.dumps(decode_config(256, 200, 80, 4, iters=10)), flush=True)
     print(json.dumps(fwd_bwd_config("configs[4]", 64, 2000, 400, iters=3, cpu_sample=16)), flush=True)
+    print(json.dumps(v2_decode_config(64, 400, 2000, 16, 4, iters=10)), flush=True)
+    print(json.dumps(tone_decode_config(64, 400, 5, 4, iters=10)), flush=True)
+    print(json.dumps({"host": HOST}), flush=True)
