@@ -343,6 +343,8 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
   const size_t simple_head = (size_t)(64 * K + 2) * sizeof(xf);
   const size_t head = simple_head > stream_head_bytes(K, U, true) ? simple_head : stream_head_bytes(K, U, true);
   const size_t rows = (size_t)T * U * sizeof(xf);
+  // the long-row kernel keeps its rows (plus beta at the cut) in the workspace at every T
+  if (U > 256) return fwd_bwd_wide_workspace_bytes(B, T, U);
   if (head + rows <= kLdsBudget) return 0;
   return (size_t)B * rows;
 }
@@ -375,10 +377,12 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
     x.exp = ee ? atoi(ee) : 0;
 #endif
     if (!a.sum_state) x.loss_sum = nullptr;
-    const int rc = launch_fwd_bwd_stream(x, st);
+    int rc = launch_fwd_bwd_stream(x, st);
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;
     summed = false;
+    rc = launch_fwd_bwd_wide(a, st);  // long rows (loss sum: the separate pass)
+    if (rc != SSNT_ERR_UNSUPPORTED) return rc;
   }
   FwdBwdArgs x = a;
   x.loss_sum = nullptr;  // the two-wave kernel only writes loss[]

@@ -112,9 +112,9 @@ def test_config2_full_size_bit_exact(gpu, oracle):
     assert np.max(np.abs(occ - 1.0)) < 1e-4
 
 
-def test_config5_long_form_properties(gpu, oracle):
-    # BASELINE configs[4] fwd-bwd: B=64 T=2000 U=400. Bit-exact on a sample of utterances,
-    # posterior-mass property on all of them.
+def test_config5_long_form_bit_exact(gpu, oracle):
+    # BASELINE configs[4] fwd-bwd: B=64 T=2000 U=400, bit-exact on every utterance, plus the
+    # posterior-mass property
     B, T, U = 64, 2000, 400
     lt = oracle.synth_log_trans(B, T, U, seed=4)
     S, P = [T] * B, [U] * B
@@ -122,9 +122,44 @@ def test_config5_long_form_properties(gpu, oracle):
     occ = -g["grad"][:, :T - 1].sum(axis=(2, 3))
     assert np.all(np.isfinite(g["loss"]))
     assert np.max(np.abs(occ - 1.0)) < 1e-3
-    pick = [0, 17, 63]
-    o = oracle.fwd_bwd_xf(lt[pick], [T] * 3, [U] * 3)
-    _assert_bit_exact({k: g[k][pick] for k in ("loss", "grad")}, o, ["loss", "grad"])
+    o = oracle.fwd_bwd_xf(lt, S, P)
+    _assert_bit_exact(g, o, ["loss", "grad"])
+
+
+WIDE_SHAPES = [  # the long-row kernel (256 < U <= 512): 3 and 4 waves per direction, odd U
+    (2, 40, 257), (3, 33, 300), (2, 50, 383), (2, 41, 384), (3, 64, 400), (2, 29, 401), (2, 36, 512),
+]
+
+
+@pytest.mark.parametrize("shape", WIDE_SHAPES)
+@pytest.mark.parametrize("obs", [False, True])
+def test_wide_rows_bit_exact(gpu, oracle, shape, obs):
+    B, T, U = shape
+    rng = np.random.default_rng(U + T)
+    lt = oracle.synth_log_trans(B, T, U, seed=U)
+    lo = (rng.standard_normal((B, T, U)) * 15 - 40).astype(np.float32) if obs else None
+    P = [min(U, T)] + [int(x) for x in rng.integers(1, min(U, T) + 1, size=B - 1)]
+    S = [T] + [int(rng.integers(p, T + 1)) for p in P[1:]]
+    g = _run_gpu(gpu, lt, S, P, lo)
+    o = oracle.fwd_bwd_xf(lt, S, P, log_obs=lo, debug=True)
+    keys = ["loss", "grad", "log_alpha", "log_beta"] + (["grad_obs"] if obs else [])
+    _assert_bit_exact(g, o, keys)
+
+
+@pytest.mark.parametrize("flags", [F_TERM, 0, F_TERM | F_ZINF])
+def test_wide_rows_edges(gpu, oracle, flags):
+    # single cell, S == P (one path), S < P (infeasible), S = 1, 2, 3 (cut at 0 / 1), a blocked
+    # lattice (Z = 0), and lengths that end inside the first / last segment
+    B, T, U = 10, 300, 300
+    rng = np.random.default_rng(7)
+    lt = oracle.synth_log_trans(B, T, U, seed=7)
+    S = np.array([1, 280, 10, 1, 2, 3, 300, 300, 129, 257])
+    P = np.array([1, 280, 12, 1, 2, 2, 300, 70, 128, 257])
+    lt[7, :, :, 0] = -np.inf  # no emits and P < S: Z = 0
+    lt[7, :, :, 1] = -np.inf
+    g = _run_gpu(gpu, lt, S, P, flags=flags)
+    o = oracle.fwd_bwd_xf(lt, S, P, flags=flags, debug=True)
+    _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
 
 
 def test_host_pointer_entry(gpu, oracle):
