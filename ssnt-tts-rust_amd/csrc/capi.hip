@@ -495,6 +495,9 @@ int ssnt_set_host_staging(int mode) {
   return g_host_mode.exchange(mode);
 }
 
+// A/B of the long-row kernel's lane width (tools, tests); not part of the public header.
+int ssnt_fwd_bwd_wide_lanes(int k) { return set_fwd_bwd_wide_lanes(k); }
+
 // diagnostic builds (make lib-diag) only; not part of the public header
 int ssnt_diag_read(void* host, size_t bytes) { return diag_read(host, bytes); }
 

@@ -23,6 +23,7 @@
 //     The kernel boundary between them is the only inter-workgroup synchronisation.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <type_traits>
 #include <utility>
 
@@ -31,11 +32,13 @@
 namespace ssnt {
 namespace {
 
-constexpr int kSeg = 128;      // positions per wave (2 per lane)
-constexpr int kBS = 8;         // steps per hand-off block (= prefetch depth: ring indices static)
-constexpr int kRB = 32;        // hand-off ring slots (steps) per wave
-constexpr int kDepth = kBS;    // rows in flight per wave
-constexpr int kMaxNW = 4;      // waves per direction: U <= 512
+// steps per hand-off block = rows in flight per wave (ring indices static). At K = 1, 16 rows of
+// 512 B per wave keep ~2 us of HBM latency covered at a ~0.2 us step (Little's law: 8 rows held
+// the kernel near 3 TB/s); K = 2 has twice the bytes per row and the registers for 8.
+template <int K>
+constexpr int block_steps() { return K == 1 ? 16 : 8; }
+constexpr int kRB = 64;        // hand-off ring slots (steps) per wave
+constexpr int kMaxNW = 8;      // waves per direction: U <= 512 (K = 1) / 1024 (K = 2)
 constexpr int kSpinMax = 1 << 22;
 
 struct WideCtl {
@@ -44,6 +47,7 @@ struct WideCtl {
   xf zpart[kMaxNW];     // per-segment sums of alpha[M] * beta[M]
   xf z;
   xf bnd[kMaxNW][kRB];  // hand-off rings
+  xf junk[kMaxNW][64];  // where the lanes that do not publish write (branch-free publication)
 };
 
 // compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>)
@@ -60,8 +64,11 @@ __device__ __forceinline__ int wctr_ld(const int* p) {
   return __builtin_amdgcn_readfirstlane(
       __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
+// a plain LDS store (the address space spelled out: a volatile or atomic store through a generic
+// pointer can become a flat store, whose completion the compiler then waits for with vmcnt(0))
+typedef __attribute__((address_space(3))) int lds_int;
 __device__ __forceinline__ void wctr_st(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  *reinterpret_cast<lds_int*>(reinterpret_cast<size_t>(p) & 0xffffffffu) = v;
 }
 // compiler-only barrier: LDS data and counter accesses stay in program order (a wave's DS
 // instructions execute in order, so "write data, then counter" publishes without a wait)
@@ -79,19 +86,28 @@ __device__ __forceinline__ void wait_ge(const int* p, int target, int* status) {
   }
 }
 
-struct WItem {  // one row's inputs for this lane's two positions
-  float lt[4];  // emit/shift of p0, p0+1
-  float ob[2];  // log_obs of the entering row (OBS)
+template <int K>
+struct WItem {    // one row's inputs for this lane's K positions
+  float lt[2 * K];  // emit/shift of p0 .. p0+K-1
+  float ob[K];      // log_obs of the entering row (OBS)
 };
-struct WRows {  // phase-2 workspace rows for this lane
-  float r0[4];  // alpha: beta[s+1]; beta: alpha[s]        (m, e, m, e)
-  float r1[4];  // alpha: beta[s] (grad_obs)
-  float nb[2];  // alpha: beta[s+1] at p0+2 (lane 63: next segment's first position)
-  float nob;    // alpha: log_obs[s+1] at p0+2
+template <int K>
+struct WRows {    // phase-2 workspace rows for this lane
+  float r0[2 * K];  // alpha: beta[s+1]; beta: alpha[s]        (m, e, m, e, ...)
+  float r1[2 * K];  // alpha: beta[s] (grad_obs)
+  float nb[2];      // alpha: beta[s+1] at p0+K (lane 63: next segment's first position)
+  float nob;        // alpha: log_obs[s+1] at p0+K
 };
 
-template <bool OBS, int PHASE>
+// DBG: log-alpha / log-beta outputs requested (a separate instantiation, so the product path's
+// step bodies carry no debug branches: straight-line blocks keep the compiler's memory wait
+// counts exact, and a wait for row r+8's loads does not drain the stores issued since)
+// K: positions per lane; a wave owns 64K consecutive positions.
+template <int K, bool OBS, int PHASE, bool DBG>
 __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
+  constexpr int kSeg = 64 * K;
+  constexpr int kBS = block_steps<K>();
+  constexpr int kDepth = kBS;  // rows in flight per wave
   __shared__ WideCtl ctl;
   const int b = blockIdx.x;
   const int dir = blockIdx.y;  // 0 alpha, 1 beta
@@ -109,10 +125,10 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   const float* lo = OBS ? a.log_obs + (size_t)b * TU : nullptr;
   float* g = a.grad ? a.grad + (size_t)b * TU * 2 : nullptr;
   float* go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
-  float* la = a.log_alpha ? a.log_alpha + (size_t)b * TU : nullptr;
-  float* lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
+  float* la = (DBG && a.log_alpha) ? a.log_alpha + (size_t)b * TU : nullptr;
+  float* lb = (DBG && a.log_beta) ? a.log_beta + (size_t)b * TU : nullptr;
   xf* rows = reinterpret_cast<xf*>(a.workspace) + (size_t)b * (T + 1) * U;  // row T: beta[M]
-  const int p0 = kSeg * w + 2 * lane;
+  const int p0 = kSeg * w + K * lane;
   const unsigned rowb = (unsigned)U * 8u, rowf = (unsigned)U * 4u;
 
   if (threadIdx.x < 2 * kMaxNW) reinterpret_cast<int*>(&ctl)[threadIdx.x] = 0;
@@ -124,45 +140,64 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   auto st_pair = [&](float* base, unsigned bytes, int off, float x0, float x1) __attribute__((always_inline)) {
     rbuf_st2(f32x2{x0, x1}, brsrc(base, bytes), off, 0, 0);
   };
-  auto put_grad = [&](int s, const float* ge, const float* gs) __attribute__((always_inline)) {
+  // Stores take a `live` flag: a dead step (past the end of the last, partial block) runs the
+  // same straight-line code but its descriptors cover 0 bytes, so its stores are dropped.
+  auto put_grad = [&](int s, const float* ge, const float* gs, bool live = true) __attribute__((always_inline)) {
     if (!g) return;
     float* row = g + (size_t)uni(s) * U * 2;
-    st_pair(row, rowb, p0 * 8, ge[0], gs[0]);
-    st_pair(row, rowb, p0 * 8 + 8, ge[1], gs[1]);
+#pragma unroll
+    for (int j = 0; j < K; ++j) st_pair(row, live ? rowb : 0u, (p0 + j) * 8, ge[j], gs[j]);
   };
-  auto put_f = [&](float* base, int s, const float* v) __attribute__((always_inline)) {  // grad_obs / debug rows
-    const __amdgpu_buffer_rsrc_t r = brsrc(base + (size_t)uni(s) * U, rowf);
-    rbuf_st1(v[0], r, p0 * 4, 0, 0);
-    rbuf_st1(v[1], r, p0 * 4 + 4, 0, 0);
+  auto put_f = [&](float* base, int s, const float* v, bool live = true) __attribute__((always_inline)) {
+    const bool on = live && base != nullptr;  // a null base (output not requested): 0 bytes
+    const __amdgpu_buffer_rsrc_t r = brsrc(on ? base + (size_t)uni(s) * U : nullptr, on ? rowf : 0u);
+#pragma unroll
+    for (int j = 0; j < K; ++j) rbuf_st1(v[j], r, (p0 + j) * 4, 0, 0);
   };
-  auto put_log = [&](float* base, int s, const XRow<2>& x) __attribute__((always_inline)) {
-    const float v[2] = {xf_log(xf{x.m[0], x.e[0]}), xf_log(xf{x.m[1], x.e[1]})};
-    put_f(base, s, v);
+  auto put_log = [&](float* base, int s, const XRow<K>& x, bool live = true) __attribute__((always_inline)) {
+    float v[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = xf_log(xf{x.m[j], x.e[j]});
+    put_f(base, s, v, live);
   };
   // workspace row s (s == T: the cut row). The fields go through registers one by one: a vector
   // built straight from the adjacent fields of the row makes the compiler keep the row in memory
-  auto put_row = [&](int s, const XRow<2>& x) __attribute__((always_inline)) {
-    float m0 = x.m[0], m1 = x.m[1];
-    int e0 = x.e[0], e1 = x.e[1];
-    asm volatile("" : "+v"(m0), "+v"(m1), "+v"(e0), "+v"(e1));
-    const __amdgpu_buffer_rsrc_t r = brsrc(rows + (size_t)uni(s) * U, rowb);
-    rbuf_st2(f32x2{m0, __builtin_bit_cast(float, e0)}, r, p0 * 8, 0, 0);
-    rbuf_st2(f32x2{m1, __builtin_bit_cast(float, e1)}, r, p0 * 8 + 8, 0, 0);
+  auto put_row = [&](int s, const XRow<K>& x, bool live = true) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t r = brsrc(rows + (size_t)uni(s) * U, live ? rowb : 0u);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      float mj = x.m[j];
+      int ej = x.e[j];
+      asm volatile("" : "+v"(mj), "+v"(ej));
+      rbuf_st2(f32x2{mj, __builtin_bit_cast(float, ej)}, r, (p0 + j) * 8, 0, 0);
+    }
   };
-  auto ld_row = [&](int s, float* v) __attribute__((always_inline)) {  // 4 floats; past U: zeros (exponent fixed by callers)
+  auto ld_row = [&](int s, float* v) __attribute__((always_inline)) {  // 2K floats; past U: zeros
     const __amdgpu_buffer_rsrc_t r = brsrc(rows + (size_t)uni(s) * U, rowb);
-    const f32x2 x = rbuf_ld2(r, p0 * 8, 0, 0), y = rbuf_ld2(r, p0 * 8 + 8, 0, 0);
-    v[0] = x.x; v[1] = x.y; v[2] = y.x; v[3] = y.y;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const f32x2 x = rbuf_ld2(r, (p0 + j) * 8, 0, 0);
+      v[2 * j] = x.x;
+      v[2 * j + 1] = x.y;
+    }
   };
   auto unpack = [&](const float* v) __attribute__((always_inline)) {
-    XRow<2> x;
-    x.m[0] = v[0]; x.e[0] = __builtin_bit_cast(int, v[1]);
-    x.m[1] = v[2]; x.e[1] = __builtin_bit_cast(int, v[3]);
+    XRow<K> x;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      x.m[j] = v[2 * j];
+      x.e[j] = __builtin_bit_cast(int, v[2 * j + 1]);
+    }
     return x;
   };
   // zero gradients, -inf debug rows (rows [from, to)); each wave writes its own segment
   auto zero_rows = [&](int from, int to) __attribute__((always_inline)) {
-    const float z[2] = {0.0f, 0.0f}, ninf[2] = {-__builtin_inff(), -__builtin_inff()};
+    float z[K], ninf[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      z[j] = 0.0f;
+      ninf[j] = -__builtin_inff();
+    }
     for (int s = from; s < to; ++s) {
       put_grad(s, z, z);
       if (go) put_f(go, s, z);
@@ -183,27 +218,43 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   }
   const int M = (S - 1) >> 1;
 
-  auto load_item = [&](int row, WItem& it) __attribute__((always_inline)) {
+  auto load_item = [&](int row, WItem<K>& it) __attribute__((always_inline)) {
     row = uni(min(max(row, 0), T - 1));
     const __amdgpu_buffer_rsrc_t r = brsrc(lt + (size_t)row * U * 2, rowb);
-    const f32x2 x = rbuf_ld2(r, p0 * 8, 0, 0), y = rbuf_ld2(r, p0 * 8 + 8, 0, 0);
-    it.lt[0] = x.x; it.lt[1] = x.y; it.lt[2] = y.x; it.lt[3] = y.y;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const f32x2 x = rbuf_ld2(r, (p0 + j) * 8, 0, 0);
+      it.lt[2 * j] = x.x;
+      it.lt[2 * j + 1] = x.y;
+    }
     if constexpr (OBS) {
       const __amdgpu_buffer_rsrc_t o = brsrc(lo + (size_t)uni(min(row + 1, T - 1)) * U, rowf);
-      it.ob[0] = rbuf_ld1(o, p0 * 4, 0, 0);
-      it.ob[1] = rbuf_ld1(o, p0 * 4 + 4, 0, 0);
+#pragma unroll
+      for (int j = 0; j < K; ++j) it.ob[j] = rbuf_ld1(o, (p0 + j) * 4, 0, 0);
     }
   };
-  auto convert2 = [&](const WItem& it, XRow<2>& E, XRow<2>& Sh, XRow<2>& O) __attribute__((always_inline)) {
+  auto convert2 = [&](const WItem<K>& it, XRow<K>& E, XRow<K>& Sh, XRow<K>& O) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < K; ++j)
       xf_exp_pair(it.lt[2 * j], it.lt[2 * j + 1], p0 + j < P, p0 + j < P - 1, E.m[j], E.e[j],
                   Sh.m[j], Sh.e[j]);
     if constexpr (OBS) {
-      xf_exp_pair(it.ob[0], it.ob[1], p0 < P, p0 + 1 < P, O.m[0], O.e[0], O.m[1], O.e[1]);
+      if constexpr (K == 1) {
+        const xf o = xf_exp(it.ob[0], p0 < P);
+        O.m[0] = o.m;
+        O.e[0] = o.e;
+      } else {
+#pragma unroll
+        for (int j = 0; j + 1 < K; j += 2)
+          xf_exp_pair(it.ob[j], it.ob[j + 1], p0 + j < P, p0 + j + 1 < P, O.m[j], O.e[j],
+                      O.m[j + 1], O.e[j + 1]);
+      }
     } else {
-      O.m[0] = O.m[1] = 1.0f;
-      O.e[0] = O.e[1] = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        O.m[j] = 1.0f;
+        O.e[j] = 0;
+      }
     }
   };
 
@@ -217,36 +268,32 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   // constant (register ring indices), (bm, be) the upstream value of iteration i and (pm, pe)
   // the value this wave hands on. The downstream wave runs at least one block behind.
   auto pipeline = [&](int n, auto&& step) __attribute__((always_inline)) {
+    // the lanes that do not publish write to their own junk slot: publication is branch-free
+    const bool pub = has_dn && lane == pub_lane;
     for (int i0 = 0; i0 < n; i0 += kBS) {
       const int i1 = min(i0 + kBS, n);
       float bm[kBS];
       int be[kBS];
-      if (has_up) {
-        wait_ge(&ctl.prod[up], i1, a.status);
-        wbar();
-#pragma unroll
-        for (int k = 0; k < kBS; ++k) {
-          const xf v = ctl.bnd[up][(i0 + k) % kRB];
-          bm[k] = v.m;
-          be[k] = v.e;
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < kBS; ++k) {
-          bm[k] = 0.0f;
-          be[k] = XF_EZERO;
-        }
-      }
+      if (has_up) wait_ge(&ctl.prod[up], i1, a.status);
       if (has_dn) wait_ge(&ctl.cons[dn], i1 - kRB, a.status);
       wbar();
+      const xf* rd = &ctl.bnd[has_up ? up : w][i0 % kRB];
+#pragma unroll
+      for (int k = 0; k < kBS; ++k) {  // (stale values when there is no upstream: unused)
+        const xf v = rd[k];
+        bm[k] = has_up ? v.m : 0.0f;
+        be[k] = has_up ? v.e : XF_EZERO;
+      }
+      xf* wp = pub ? &ctl.bnd[w][i0 % kRB] : &ctl.junk[w][lane];
+      const int ws = pub ? 1 : 0;
+      // one straight-line path for every block (steps past n are dead: their stores are
+      // dropped): no join of two paths, so no register copies of rows with loads in flight
       sfor<kBS>([&](auto Kc) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
-        if (i0 + k < i1) {
-          float pm;
-          int pe;
-          step(i0 + k, Kc, bm[k], be[k], pm, pe);
-          if (has_dn && lane == pub_lane) ctl.bnd[w][(i0 + k) % kRB] = xf{pm, pe};
-        }
+        float pm;
+        int pe;
+        step(i0 + k, Kc, bm[k], be[k], pm, pe, i0 + k < i1);
+        wp[k * ws] = xf{pm, pe};
       });
       wbar();
       if (has_dn) wctr_st(&ctl.prod[w], i1);
@@ -256,26 +303,26 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
 
   // alpha[r+1] from alpha[r] (= A); (bm, be): the left segment's shift product of its last
   // position; hands on this segment's. The operations of lattice_dev.h alpha_step.
-  auto alpha_next = [&](XRow<2>& A, const XRow<2>& E, const XRow<2>& Sh, const XRow<2>& O,
+  auto alpha_next = [&](XRow<K>& A, const XRow<K>& E, const XRow<K>& Sh, const XRow<K>& O,
                         float bm, int be, float& pm, int& pe) __attribute__((always_inline)) {
-    XRow<2> st, sh;
+    XRow<K> st, sh;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < K; ++j) {
       st.m[j] = A.m[j] * E.m[j];
       st.e[j] = A.e[j] + E.e[j];
       sh.m[j] = A.m[j] * Sh.m[j];
       sh.e[j] = A.e[j] + Sh.e[j];
     }
-    pm = sh.m[1];
-    pe = sh.e[1];
-    float lm = shr1(sh.m[1]);
-    int le = shr1(sh.e[1]);
+    pm = sh.m[K - 1];
+    pe = sh.e[K - 1];
+    float lm = shr1(sh.m[K - 1]);
+    int le = shr1(sh.e[K - 1]);
     lm = lane == 0 ? bm : lm;
     le = lane == 0 ? be : le;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float hm = j == 0 ? lm : sh.m[0];
-      const int he = j == 0 ? le : sh.e[0];
+    for (int j = 0; j < K; ++j) {
+      const float hm = j == 0 ? lm : sh.m[j > 0 ? j - 1 : 0];
+      const int he = j == 0 ? le : sh.e[j > 0 ? j - 1 : 0];
       const int em = max(st.e[j], he);
       float sum = xldexp(st.m[j], st.e[j] - em) + xldexp(hm, he - em);
       int ee = em;
@@ -290,10 +337,10 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   };
   // Q = beta[s+1] (x obs[s+1]) and R = Q[p+1]; (bm, be): the right segment's Q of its first
   // position; hands on this segment's. The operations of lattice_dev.h entering.
-  auto entering2 = [&](const XRow<2>& X, const XRow<2>& O, float bm, int be, XRow<2>& Q,
-                       XRow<2>& R, float& pm, int& pe) __attribute__((always_inline)) {
+  auto entering2 = [&](const XRow<K>& X, const XRow<K>& O, float bm, int be, XRow<K>& Q,
+                       XRow<K>& R, float& pm, int& pe) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < K; ++j) {
       Q.m[j] = OBS ? X.m[j] * O.m[j] : X.m[j];
       Q.e[j] = OBS ? X.e[j] + O.e[j] : X.e[j];
     }
@@ -303,22 +350,23 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
     int re = shl1(Q.e[0]);
     rm = lane == 63 ? bm : rm;
     re = lane == 63 ? be : re;
-    R.m[0] = Q.m[1];
-    R.e[0] = Q.e[1];
-    R.m[1] = rm;
-    R.e[1] = re;
-  };
-  auto beta_next = [&](XRow<2>& X, const XRow<2>& E, const XRow<2>& Sh, const XRow<2>& Q,
-                       const XRow<2>& R) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < K; ++j) {
+      R.m[j] = j == K - 1 ? rm : Q.m[j + 1 < K ? j + 1 : 0];
+      R.e[j] = j == K - 1 ? re : Q.e[j + 1 < K ? j + 1 : 0];
+    }
+  };
+  auto beta_next = [&](XRow<K>& X, const XRow<K>& E, const XRow<K>& Sh, const XRow<K>& Q,
+                       const XRow<K>& R) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
       const xf r = xf_add(E.m[j] * Q.m[j], E.e[j] + Q.e[j], Sh.m[j] * R.m[j], Sh.e[j] + R.e[j]);
       X.m[j] = r.m;
       X.e[j] = r.e;
     }
   };
 
-  WItem ring[kDepth];
+  WItem<K> ring[kDepth];
   if constexpr (PHASE == 1) {
     if (dir == 0) {
       // ---------------- alpha[0..M]: rows 0..M of the workspace ----------------
@@ -330,33 +378,36 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
         a0 = xf_norm(o.m, o.e);
       }
       const bool first = w == 0 && lane == 0;
-      XRow<2> X;  // alpha row of this lane's two positions
+      XRow<K> X;  // alpha row of this lane's K positions
       X.m[0] = first ? a0.m : 0.0f;
       X.e[0] = first ? a0.e : XF_EZERO;
-      X.m[1] = 0.0f;
-      X.e[1] = XF_EZERO;
+#pragma unroll
+      for (int j = 1; j < K; ++j) {
+        X.m[j] = 0.0f;
+        X.e[j] = XF_EZERO;
+      }
       put_row(0, X);
-      if (la) put_log(la, 0, X);
+      if constexpr (DBG) { if (la) put_log(la, 0, X); }
 #pragma unroll
       for (int k = 0; k < kDepth; ++k) load_item(k, ring[k]);
-      pipeline(M, [&](int r, auto Kc, float bm, int be, float& pm, int& pe) __attribute__((always_inline)) {
+      pipeline(M, [&](int r, auto Kc, float bm, int be, float& pm, int& pe, bool live) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
-        XRow<2> E, Sh, O;
+        XRow<K> E, Sh, O;
         convert2(ring[k], E, Sh, O);
         load_item(r + kDepth, ring[k]);
         alpha_next(X, E, Sh, O, bm, be, pm, pe);
-        put_row(r + 1, X);
-        if (la) put_log(la, r + 1, X);
+        put_row(r + 1, X, live);
+        if constexpr (DBG) put_log(la, r + 1, X, live);
       });
     } else {
       // ---------------- beta[S-1..M]: rows S-1..M+1, beta[M] to row T ----------------
-      XRow<2> X;  // beta row of this lane's two positions
+      XRow<K> X;  // beta row of this lane's K positions
       load_item(S - 1, ring[0]);
       {
-        XRow<2> E, Sh, O;
+        XRow<K> E, Sh, O;
         convert2(ring[0], E, Sh, O);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {  // terminal emit (src/lib.rs:187-195)
+        for (int j = 0; j < K; ++j) {  // terminal emit (src/lib.rs:187-195)
           const bool last = p0 + j == P - 1;
           const xf v = term ? xf_norm(E.m[j], E.e[j]) : xf{0.5f, 1};
           X.m[j] = last ? v.m : 0.0f;
@@ -364,37 +415,47 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
         }
       }
       put_row(S - 1 > M ? S - 1 : T, X);
-      if (lb) put_log(lb, S - 1, X);
+      if constexpr (DBG) { if (lb) put_log(lb, S - 1, X); }
 #pragma unroll
       for (int k = 0; k < kDepth; ++k) load_item(S - 2 - k, ring[k]);
-      pipeline(S - 1 - M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe) __attribute__((always_inline)) {
+      pipeline(S - 1 - M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe, bool live) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
         const int s = S - 2 - i;
-        XRow<2> E, Sh, O, Q, R;
+        XRow<K> E, Sh, O, Q, R;
         convert2(ring[k], E, Sh, O);  // E, Sh of row s; O of row s+1
         load_item(s - kDepth, ring[k]);
         entering2(X, O, bm, be, Q, R, pm, pe);
         beta_next(X, E, Sh, Q, R);
-        put_row(s > M ? s : T, X);
-        if (lb) put_log(lb, s, X);
+        put_row(s > M ? s : T, X, live);
+        if constexpr (DBG) put_log(lb, s, X, live);
       });
     }
     return;
   } else {
     // ---------------- phase 2: Z at the cut (both workgroups, the oracle's tree) ----------------
-    float v[4], u[4];
+    float v[2 * K], u[2 * K];
     ld_row(M, v);
     ld_row(T, u);
-    float wm[2];
-    int we[2];
+    float wm[K];
+    int we[K];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < K; ++j) {
       const bool live = p0 + j < P;
       wm[j] = live ? v[2 * j] * u[2 * j] : 0.0f;
       we[j] = live ? __builtin_bit_cast(int, v[2 * j + 1]) + __builtin_bit_cast(int, u[2 * j + 1])
                    : XF_EZERO;
     }
-    xf z = xf_add(wm[0], we[0], wm[1], we[1]);
+    // in-lane levels of the oracle's tree (pairs (2i, 2i+1) first), then across lanes and waves
+#pragma unroll
+    for (int len = K; len > 1; len >>= 1) {
+#pragma unroll
+      for (int q = 0; q < len / 2; ++q) {
+        const xf t2 = xf_add(wm[2 * q], we[2 * q], wm[2 * q + 1], we[2 * q + 1]);
+        wm[q] = t2.m;
+        we[q] = t2.e;
+      }
+    }
+    xf z{wm[0], we[0]};
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const float om = __shfl_xor(z.m, off);
@@ -426,43 +487,44 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
     if (dir == 0 && threadIdx.x == 0) a.loss[b] = 0.0f - xf_log(Z);
     const float izm = 1.0f / Z.m;
     const int ize = -Z.e;
-    WRows wr[kDepth];
+    WRows<K> wr[kDepth];
     if (dir == 0) {
       // ---------------- alpha: rows M..S-1, gradient rows s >= M ----------------
-      auto load_rows = [&](int s, WRows& r) __attribute__((always_inline)) {  // beta[s+1] (+ its position p0+2), beta[s]
+      auto load_rows = [&](int s, WRows<K>& r) __attribute__((always_inline)) {  // beta[s+1] (+ position p0+K), beta[s]
         const int sn = uni(min(s + 1, S - 1));
         ld_row(sn, r.r0);
         const __amdgpu_buffer_rsrc_t rr = brsrc(rows + (size_t)sn * U, rowb);
-        const f32x2 x = rbuf_ld2(rr, p0 * 8 + 16, 0, 0);
+        const f32x2 x = rbuf_ld2(rr, (p0 + K) * 8, 0, 0);
         r.nb[0] = x.x;
         r.nb[1] = x.y;
         if constexpr (OBS) {
           ld_row(s == M ? T : min(s, S - 1), r.r1);
-          r.nob = rbuf_ld1(brsrc(lo + (size_t)uni(min(s + 1, T - 1)) * U, rowf), p0 * 4 + 8, 0, 0);
+          r.nob = rbuf_ld1(brsrc(lo + (size_t)uni(min(s + 1, T - 1)) * U, rowf), (p0 + K) * 4, 0, 0);
         }
       };
       ld_row(M, v);
-      XRow<2> X = unpack(v);
+      XRow<K> X = unpack(v);
 #pragma unroll
       for (int k = 0; k < kDepth; ++k) {
         load_item(M + k, ring[k]);
         load_rows(M + k, wr[k]);
       }
-      pipeline(S - M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe) __attribute__((always_inline)) {
+      pipeline(S - M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe, bool live) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
         const int s = M + i;
-        XRow<2> E, Sh, O, Q, R;
+        const bool fin = s + 1 >= S;  // the terminal transition (selects, not a branch)
+        XRow<K> E, Sh, O, Q, R;
         convert2(ring[k], E, Sh, O);
-        const WRows rw = wr[k];
+        const WRows<K> rw = wr[k];
         load_item(s + kDepth, ring[k]);
         load_rows(s + kDepth, wr[k]);
-        if (s + 1 < S) {
-          XRow<2> Bn = unpack(rw.r0);
+        {
+          const XRow<K> Bn = unpack(rw.r0);
           // the right neighbour of position p0+1 (lane 63: the next segment's first position)
           float om = 1.0f;
           int oe = 0;
           if constexpr (OBS) {
-            const xf o = xf_exp(rw.nob, p0 + 2 < P);
+            const xf o = xf_exp(rw.nob, p0 + K < P);
             om = o.m;
             oe = o.e;
           }
@@ -471,87 +533,91 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
           float qm;
           int qe;
           entering2(Bn, O, nbm, nbe, Q, R, qm, qe);
-        } else {  // terminal transition: only the terminal emit at P-1 (src/lib.rs:187-195)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const bool last = term && p0 + j == P - 1;
-            Q.m[j] = last ? 1.0f : 0.0f;
-            Q.e[j] = last ? 0 : XF_EZERO;
-            R.m[j] = 0.0f;
-            R.e[j] = XF_EZERO;
-          }
         }
-        float ge[2], gs[2], gob[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < K; ++j) {  // terminal: only the terminal emit at P-1 (src/lib.rs:187-195)
+          const bool last = term && p0 + j == P - 1;
+          Q.m[j] = fin ? (last ? 1.0f : 0.0f) : Q.m[j];
+          Q.e[j] = fin ? (last ? 0 : XF_EZERO) : Q.e[j];
+          R.m[j] = fin ? 0.0f : R.m[j];
+          R.e[j] = fin ? XF_EZERO : R.e[j];
+        }
+        float ge[K], gs[K], gob[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
           ge[j] = xf_neg_post(((X.m[j] * E.m[j]) * Q.m[j]) * izm, X.e[j] + E.e[j] + Q.e[j] + ize);
           gs[j] = xf_neg_post(((X.m[j] * Sh.m[j]) * R.m[j]) * izm, X.e[j] + Sh.e[j] + R.e[j] + ize);
         }
-        put_grad(s, ge, gs);
+        put_grad(s, ge, gs, live);
         if constexpr (OBS) {
-          const XRow<2> Bs = unpack(rw.r1);
+          const XRow<K> Bs = unpack(rw.r1);
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < K; ++j)
             gob[j] = xf_neg_post((X.m[j] * Bs.m[j]) * izm, X.e[j] + Bs.e[j] + ize);
-          if (go) put_f(go, s, gob);
+          put_f(go, s, gob, live);
         }
-        if (s + 1 < S) {
-          alpha_next(X, E, Sh, O, bm, be, pm, pe);
-          if (la) put_log(la, s + 1, X);
-        } else {
-          pm = 0.0f;
-          pe = XF_EZERO;
-        }
+        // past the terminal transition X is dead (no live step follows)
+        alpha_next(X, E, Sh, O, bm, be, pm, pe);
+        if constexpr (DBG) put_log(la, s + 1, X, live && !fin);
       });
       zero_rows(S, T);  // rows past the lattice
     } else {
       // ---------------- beta: rows M-1..0, gradient rows s < M ----------------
       ld_row(T, v);
-      XRow<2> X = unpack(v);
-      auto load_rows = [&](int s, WRows& r) __attribute__((always_inline)) { ld_row(max(s, 0), r.r0); };  // alpha[s]
+      XRow<K> X = unpack(v);
+      auto load_rows = [&](int s, WRows<K>& r) __attribute__((always_inline)) { ld_row(max(s, 0), r.r0); };  // alpha[s]
 #pragma unroll
       for (int k = 0; k < kDepth; ++k) {
         load_item(M - 1 - k, ring[k]);
         load_rows(M - 1 - k, wr[k]);
       }
-      pipeline(M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe) __attribute__((always_inline)) {
+      pipeline(M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe, bool live) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
         const int s = M - 1 - i;
-        XRow<2> E, Sh, O, Q, R;
+        XRow<K> E, Sh, O, Q, R;
         convert2(ring[k], E, Sh, O);  // E, Sh of row s; O of row s+1
-        const XRow<2> A = unpack(wr[k].r0);
+        const XRow<K> A = unpack(wr[k].r0);
         load_item(s - kDepth, ring[k]);
         load_rows(s - kDepth, wr[k]);
         entering2(X, O, bm, be, Q, R, pm, pe);
-        float ge[2], gs[2], gob[2];
+        float ge[K], gs[K], gob[K];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < K; ++j) {
           ge[j] = xf_neg_post(((A.m[j] * E.m[j]) * Q.m[j]) * izm, A.e[j] + E.e[j] + Q.e[j] + ize);
           gs[j] = xf_neg_post(((A.m[j] * Sh.m[j]) * R.m[j]) * izm, A.e[j] + Sh.e[j] + R.e[j] + ize);
         }
         beta_next(X, E, Sh, Q, R);
-        put_grad(s, ge, gs);
+        put_grad(s, ge, gs, live);
         if constexpr (OBS) {
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < K; ++j)
             gob[j] = xf_neg_post((A.m[j] * X.m[j]) * izm, A.e[j] + X.e[j] + ize);
-          if (go) put_f(go, s, gob);
+          put_f(go, s, gob, live);
         }
-        if (lb) put_log(lb, s, X);
+        if constexpr (DBG) put_log(lb, s, X, live);
       });
     }
   }
 }
 
-template <bool OBS>
+template <int K, bool OBS, bool DBG>
 int launch_wide(const FwdBwdArgs& a, hipStream_t st) {
-  const int NW = (a.U + kSeg - 1) / kSeg;
+  const int NW = (a.U + 64 * K - 1) / (64 * K);
   const dim3 grid(a.B, 2), block(64 * NW);
-  hipLaunchKernelGGL((k_fwd_bwd_wide<OBS, 1>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 1, DBG>), grid, block, 0, st, a);
   if (hipGetLastError() != hipSuccess) return SSNT_ERR_HIP;
-  hipLaunchKernelGGL((k_fwd_bwd_wide<OBS, 2>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 2, DBG>), grid, block, 0, st, a);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
+
+template <int K>
+int launch_wide_k(const FwdBwdArgs& a, hipStream_t st) {
+  const bool dbg = a.log_alpha || a.log_beta;
+  if (a.log_obs) return dbg ? launch_wide<K, true, true>(a, st) : launch_wide<K, true, false>(a, st);
+  return dbg ? launch_wide<K, false, true>(a, st) : launch_wide<K, false, false>(a, st);
+}
+
+std::atomic<int> g_wide_k{1};  // positions per lane (A/B hook ssnt_fwd_bwd_wide_lanes; 1 default)
 
 }  // namespace
 
@@ -560,10 +626,17 @@ size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U) {
 }
 
 int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t st) {
-  if (a.U <= 256 || a.U > kSeg * kMaxNW) return SSNT_ERR_UNSUPPORTED;
+  if (a.U <= 256 || a.U > 64 * 2 * kMaxNW) return SSNT_ERR_UNSUPPORTED;
   if (!a.workspace || a.workspace_bytes < fwd_bwd_wide_workspace_bytes(a.B, a.T, a.U))
     return SSNT_ERR_WORKSPACE;
-  return a.log_obs ? launch_wide<true>(a, st) : launch_wide<false>(a, st);
+  const bool k1 = g_wide_k.load(std::memory_order_relaxed) == 1 && a.U <= 64 * kMaxNW;
+  return k1 ? launch_wide_k<1>(a, st) : launch_wide_k<2>(a, st);
+}
+
+int set_fwd_bwd_wide_lanes(int k) {
+  if (k != 1 && k != 2) return SSNT_ERR_INVALID_ARG;
+  g_wide_k.store(k);
+  return SSNT_OK;
 }
 
 }  // namespace ssnt

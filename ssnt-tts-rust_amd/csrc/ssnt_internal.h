@@ -47,6 +47,7 @@ void set_stream_mix(int m);  // tuning only
 // long-row kernel (fwd_bwd_wide.hip, 256 < U <= 512): SSNT_ERR_UNSUPPORTED for other shapes
 int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t stream);
 size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U);
+int set_fwd_bwd_wide_lanes(int k);  // A/B: positions per lane of the long-row kernel (1 or 2)
 size_t stream_head_bytes(int K, int U, bool obs, int ring = 0);  // LDS bytes besides the lattice rows
 int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only (tools/diag_fwd_bwd.py)
 

@@ -126,14 +126,25 @@ def test_config5_long_form_bit_exact(gpu, oracle):
     _assert_bit_exact(g, o, ["loss", "grad"])
 
 
-WIDE_SHAPES = [  # the long-row kernel (256 < U <= 512): 3 and 4 waves per direction, odd U
+@pytest.fixture(params=[1, 2], ids=["K1", "K2"])
+def wide_lanes(request, gpu):
+    """The long-row kernel's two lane widths (positions per lane) must be bit-identical."""
+    import ctypes
+    lib = gpu.load()
+    lib.ssnt_fwd_bwd_wide_lanes.restype = ctypes.c_int
+    assert lib.ssnt_fwd_bwd_wide_lanes(request.param) == 0
+    yield request.param
+    lib.ssnt_fwd_bwd_wide_lanes(1)
+
+
+WIDE_SHAPES = [  # the long-row kernel (256 < U <= 512): 3..8 waves per direction, odd U
     (2, 40, 257), (3, 33, 300), (2, 50, 383), (2, 41, 384), (3, 64, 400), (2, 29, 401), (2, 36, 512),
 ]
 
 
 @pytest.mark.parametrize("shape", WIDE_SHAPES)
 @pytest.mark.parametrize("obs", [False, True])
-def test_wide_rows_bit_exact(gpu, oracle, shape, obs):
+def test_wide_rows_bit_exact(gpu, oracle, wide_lanes, shape, obs):
     B, T, U = shape
     rng = np.random.default_rng(U + T)
     lt = oracle.synth_log_trans(B, T, U, seed=U)
@@ -147,7 +158,7 @@ def test_wide_rows_bit_exact(gpu, oracle, shape, obs):
 
 
 @pytest.mark.parametrize("flags", [F_TERM, 0, F_TERM | F_ZINF])
-def test_wide_rows_edges(gpu, oracle, flags):
+def test_wide_rows_edges(gpu, oracle, wide_lanes, flags):
     # single cell, S == P (one path), S < P (infeasible), S = 1, 2, 3 (cut at 0 / 1), a blocked
     # lattice (Z = 0), and lengths that end inside the first / last segment
     B, T, U = 10, 300, 300

@@ -13,6 +13,10 @@ import ssnt_tts_amd as S  # noqa: E402
 from bench import synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+if len(sys.argv) > 2:  # A/B: positions per lane of the long-row kernel
+    import ctypes
+    S.load().ssnt_fwd_bwd_wide_lanes.restype = ctypes.c_int
+    assert S.load().ssnt_fwd_bwd_wide_lanes(int(sys.argv[2])) == 0
 B, T, U = 64, 2000, 400
 dev = torch.device("cuda:0")
 lt = synth(B, T, U, 0, dev)
