@@ -121,6 +121,8 @@ def main():
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--U", type=int, default=80)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", type=int, default=0, help="fwd-bwd kernel variant (A/B; "
+                    "ssnt_fwd_bwd_set_variant): 0 default, 1 two-wave, 2 segmented")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse "
                     "the multi-rank path on a one-GPU box")
     args = ap.parse_args()
@@ -139,6 +141,8 @@ def main():
             torch.distributed.init_process_group(args.dist_backend)
 
     B, T, U = args.batch, args.T, args.U
+    if args.variant:
+        assert S.load().ssnt_fwd_bwd_set_variant(args.variant) == 0
     lt = synth(B, T, U, seed=rank, dev=dev)
     sl = torch.full((B,), T, dtype=torch.int32, device=dev)
     pl = torch.full((B,), U, dtype=torch.int32, device=dev)

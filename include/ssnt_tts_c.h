@@ -123,10 +123,11 @@ int ssnt_version(char *buf, size_t len);
  * default); `workspace` must hold ssnt_fwd_bwd_workspace_size() bytes (may be 0 -> NULL);
  * `status` (device int, may be NULL) receives error bits. Asynchronous. */
 size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos);
-/* Kernel variant for the forward-backward (results are bit-identical): 0 = streaming kernel
- * (two chain waves fed by converter waves, gradient waves behind them; default; shapes it does
- * not take fall back to 1); 1 = two-wave kernel. Process-wide; env SSNT_FWD_BWD_KERNEL=simple
- * selects 1 at first use. For A/B timing and debugging. */
+/* Kernel variant for the forward-backward (results are bit-identical): 0 = default dispatch
+ * (streaming kernel for U <= 256, segmented kernel for longer rows, two-wave kernel for what
+ * neither takes); 1 = two-wave kernel; 2 = segmented kernel at every U it takes (U <= 1024).
+ * Process-wide; env SSNT_FWD_BWD_KERNEL=simple selects 1 at first use. For A/B timing and
+ * debugging. */
 int ssnt_fwd_bwd_set_variant(int variant);
 int ssnt_fwd_bwd_device(const float *log_trans, const float *log_obs, const int *step_len,
                         const int *pos_len, int batch, int max_steps, int max_pos, int flags,

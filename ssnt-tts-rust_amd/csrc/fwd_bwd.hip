@@ -337,28 +337,22 @@ int variant() {
 }  // namespace
 
 size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
-  // rows go to global memory when they do not fit LDS beside the largest LDS head of either
-  // kernel (with or without log_obs): conservative, so one size serves every variant
-  const int K = U <= 64 ? 1 : U <= 128 ? 2 : U <= 256 ? 4 : 8;
-  const size_t simple_head = (size_t)(64 * K + 2) * sizeof(xf);
-  const size_t head = simple_head > stream_head_bytes(K, U, true) ? simple_head : stream_head_bytes(K, U, true);
-  const size_t rows = (size_t)T * U * sizeof(xf);
-  // the long-row kernel keeps its rows (plus beta at the cut) in the workspace at every T
-  if (U > 256) return fwd_bwd_wide_workspace_bytes(B, T, U);
-  if (head + rows <= kLdsBudget) return 0;
-  return (size_t)B * rows;
+  // the segmented kernel keeps its rows (plus beta at the cut) in the workspace at every T; one
+  // size serves every kernel variant (the two-wave kernel needs B*T*U xf at most)
+  return fwd_bwd_wide_workspace_bytes(B, T, U);
 }
 
 int set_fwd_bwd_variant(int v) {
-  // 0 stream, 1 two-wave; 2..10 (SSNT_EXP builds only): stream with another wave mix / ring /
+  // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel (fwd_bwd_wide.hip) at every U it
+  // takes; 3..11 (SSNT_EXP builds only): streaming kernel with another wave mix / ring /
   // publication period (tuning)
-  if (v < 0 || v > 10) return SSNT_ERR_INVALID_ARG;
+  if (v < 0 || v > 11) return SSNT_ERR_INVALID_ARG;
 #ifndef SSNT_EXP
-  if (v >= 2) return SSNT_ERR_UNSUPPORTED;
+  if (v >= 3) return SSNT_ERR_UNSUPPORTED;
 #endif
   variant();  // the environment is read once, before any explicit choice
-  g_variant.store(v >= 2 ? 0 : v);
-  set_stream_mix(v >= 2 ? v - 1 : 0);
+  g_variant.store(v >= 3 ? 0 : v);
+  set_stream_mix(v >= 3 ? v - 2 : 0);
   return SSNT_OK;
 }
 
@@ -381,7 +375,15 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;
     summed = false;
-    rc = launch_fwd_bwd_wide(a, st);  // long rows (loss sum: the separate pass)
+    // long rows, and the shapes the streaming kernel declines (U % K != 0, offset or unaligned
+    // tensors): the segmented kernel takes any U <= 1024 at 8-byte alignment (loss sum: the
+    // separate pass)
+    if (a.workspace && a.workspace_bytes >= fwd_bwd_wide_workspace_bytes(a.B, a.T, a.U)) {
+      rc = launch_fwd_bwd_wide(a, st, true);
+      if (rc != SSNT_ERR_UNSUPPORTED) return rc;
+    }
+  } else if (variant() == 2) {
+    const int rc = launch_fwd_bwd_wide(a, st, true);
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;
   }
   FwdBwdArgs x = a;

@@ -625,8 +625,13 @@ size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U) {
   return (size_t)B * ((size_t)T + 1) * U * sizeof(xf);  // rows 0..T-1 + the cut row T
 }
 
-int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t st) {
-  if (a.U <= 256 || a.U > 64 * 2 * kMaxNW) return SSNT_ERR_UNSUPPORTED;
+int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t st, bool any_u) {
+  if ((!any_u && a.U <= 256) || a.U > 64 * 2 * kMaxNW) return SSNT_ERR_UNSUPPORTED;
+  // 8-byte granules: every tensor base must be 8-byte aligned (4 for the f32-element ones)
+  auto al = [](const void* p, uintptr_t m) { return (reinterpret_cast<uintptr_t>(p) & (m - 1)) == 0; };
+  if (!al(a.log_trans, 8) || !al(a.grad, 8) || !al(a.workspace, 8) || !al(a.log_obs, 4) ||
+      !al(a.grad_obs, 4) || !al(a.log_alpha, 4) || !al(a.log_beta, 4))
+    return SSNT_ERR_UNSUPPORTED;
   if (!a.workspace || a.workspace_bytes < fwd_bwd_wide_workspace_bytes(a.B, a.T, a.U))
     return SSNT_ERR_WORKSPACE;
   const bool k1 = g_wide_k.load(std::memory_order_relaxed) == 1 && a.U <= 64 * kMaxNW;

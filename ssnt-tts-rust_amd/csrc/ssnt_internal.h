@@ -44,8 +44,9 @@ int set_fwd_bwd_variant(int v);
 // streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t stream);
 void set_stream_mix(int m);  // tuning only
-// long-row kernel (fwd_bwd_wide.hip, 256 < U <= 512): SSNT_ERR_UNSUPPORTED for other shapes
-int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t stream);
+// segmented kernel (fwd_bwd_wide.hip): long rows (256 < U <= 1024), or any U <= 1024 when
+// any_u; SSNT_ERR_UNSUPPORTED for other shapes
+int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t stream, bool any_u);
 size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U);
 int set_fwd_bwd_wide_lanes(int k);  // A/B: positions per lane of the long-row kernel (1 or 2)
 size_t stream_head_bytes(int K, int U, bool obs, int ring = 0);  // LDS bytes besides the lattice rows

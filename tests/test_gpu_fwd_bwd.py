@@ -15,9 +15,9 @@ pytestmark = pytest.mark.gpu
 F_TERM, F_ZINF = 1, 2
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["stream", "simple"])
+@pytest.fixture(autouse=True, params=[0, 1, 2], ids=["default", "simple", "segmented"])
 def kernel_variant(request, gpu):
-    """Every parity case runs on both kernels (they must be bit-identical)."""
+    """Every parity case runs on every kernel (they must be bit-identical)."""
     lib = gpu.load()
     assert lib.ssnt_fwd_bwd_set_variant(request.param) == 0
     yield request.param
@@ -198,9 +198,9 @@ def test_autograd_function(gpu, oracle):
     assert np.array_equal(x.grad.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [3, 4, 5, 6, 7, 8, 9, 10, 11])
 def test_tuning_wave_mixes_bit_exact(gpu, oracle, kernel_variant, variant):
-    # the converter / gradient wave mixes, ring sizes and publication periods of the streaming kernel (variants 2..10,
+    # the converter / gradient wave mixes, ring sizes and publication periods of the streaming kernel (variants 3..11,
     # K = 2 shapes) must be bit-identical to the oracle like the default mix
     if kernel_variant != 0:
         pytest.skip("mix variants are streaming-kernel variants")
@@ -261,10 +261,12 @@ def test_fused_loss_sum(gpu, oracle, kernel_variant, B):
     lsum = torch.full((1,), -1.0, device=dev)
     import ctypes
     vp = ctypes.c_void_p
+    wsb = int(lib.ssnt_fwd_bwd_workspace_size(B, T, U))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
     rc = lib.ssnt_fwd_bwd_sum_device(vp(x.data_ptr()), None, vp(sl.data_ptr()), vp(pl.data_ptr()),
                                      B, T, U, F_TERM | F_ZINF, vp(loss.data_ptr()),
-                                     vp(grad.data_ptr()), None, None, None, None, 0, None,
-                                     vp(lsum.data_ptr()), None,
+                                     vp(grad.data_ptr()), None, None, None, vp(ws.data_ptr()), wsb,
+                                     None, vp(lsum.data_ptr()), None,
                                      vp(torch.cuda.current_stream(dev).cuda_stream))
     assert rc == 0
     torch.cuda.synchronize()
@@ -285,3 +287,42 @@ def test_fused_loss_sum_more_workgroups_than_cus(gpu, oracle, kernel_variant):
         r = gpu.ssnt_fwd_bwd(x, sl, pl, loss_sum=True, check=True)
         assert np.array_equal(r["loss"].cpu().numpy(), o["loss"])
         assert r["loss_sum"].cpu().numpy()[0] == _wave_order_sum(o["loss"])
+
+
+@pytest.mark.parametrize("shape", [(2, 30, 700), (2, 24, 1024), (3, 26, 777)])
+def test_rows_beyond_512_bit_exact(gpu, oracle, kernel_variant, shape):
+    # 512 < U <= 1024: only the segmented kernel (two positions per lane, 8 waves per direction)
+    # takes these; the two-wave kernel declines them
+    if kernel_variant == 1:
+        pytest.skip("the two-wave kernel stops at U = 512")
+    B, T, U = shape
+    rng = np.random.default_rng(U)
+    lt = oracle.synth_log_trans(B, T, U, seed=U)
+    P = [min(U, T)] + [int(x) for x in rng.integers(1, min(U, T) + 1, size=B - 1)]
+    S = [T] + [int(rng.integers(p, T + 1)) for p in P[1:]]
+    g = _run_gpu(gpu, lt, S, P)
+    o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
+    _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+
+
+@pytest.mark.parametrize("shift", [1, 2, 4])
+@pytest.mark.parametrize("U", [80, 81])
+def test_offset_and_odd_shapes(gpu, oracle, kernel_variant, shift, U):
+    # tensors at an element offset (4 / 8 / 16-byte aligned bases) and U % K != 0: the streaming
+    # kernel declines what it cannot vector-load and the segmented / two-wave kernels take over
+    # with identical bits
+    dev = torch.device("cuda:0")
+    B, T = 5, 70
+    lt = oracle.synth_log_trans(B, T, U, seed=shift + U)
+    rng = np.random.default_rng(shift)
+    P = [U] + [int(x) for x in rng.integers(1, U + 1, size=B - 1)]
+    S = [T] + [int(rng.integers(p, T + 1)) for p in P[1:]]
+    flat = torch.zeros(lt.size + shift, dtype=torch.float32, device=dev)
+    flat[shift:] = torch.from_numpy(lt.ravel()).to(dev)
+    x = flat[shift:].view(B, T, U, 2)
+    assert x.data_ptr() % 16 == (4 * shift) % 16
+    r = gpu.ssnt_fwd_bwd(x, torch.tensor(S, dtype=torch.int32, device=dev),
+                         torch.tensor(P, dtype=torch.int32, device=dev), debug=True, check=True)
+    g = {k: v.cpu().numpy() for k, v in r.items() if k != "status"}
+    o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
+    _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
