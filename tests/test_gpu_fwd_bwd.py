@@ -312,7 +312,7 @@ def test_offset_and_odd_shapes(gpu, oracle, kernel_variant, shift, U):
     # kernel declines what it cannot vector-load and the segmented / two-wave kernels take over
     # with identical bits
     dev = torch.device("cuda:0")
-    B, T = 5, 70
+    B, T = 5, 90
     lt = oracle.synth_log_trans(B, T, U, seed=shift + U)
     rng = np.random.default_rng(shift)
     P = [U] + [int(x) for x in rng.integers(1, U + 1, size=B - 1)]
