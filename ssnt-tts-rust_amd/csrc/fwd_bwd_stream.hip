@@ -56,8 +56,21 @@ template <bool OBS>
 constexpr int out_slots() { return OBS ? 4 : 8; }  // chain-row ring (rows past the cut) per direction
 template <bool OBS>
 constexpr int kChainPrefetch(int R) { return R >= 16 ? 4 : 2; }  // factor rows in flight per chain
+// build-time tuning overrides (tools/build_variants.sh; the product uses the defaults)
+#ifndef SSNT_T_CDEPTH
+#define SSNT_T_CDEPTH 8
+#endif
+#ifndef SSNT_T_CPRIO
+#define SSNT_T_CPRIO 0
+#endif
+#ifndef SSNT_T_NC
+#define SSNT_T_NC 3
+#endif
+#ifndef SSNT_T_NH
+#define SSNT_T_NH 4
+#endif
 template <int K>
-constexpr int conv_depth() { return K <= 2 ? 8 : (K <= 4 ? 4 : 2); }  // converter prefetch rows
+constexpr int conv_depth() { return K <= 2 ? SSNT_T_CDEPTH : (K <= 4 ? 4 : 2); }  // converter prefetch rows
 
 // experiment knobs (SSNT_EXP builds only; compiled out of the product)
 #ifdef SSNT_EXP
@@ -218,21 +231,42 @@ __device__ __forceinline__ int shl_z(int x) { return __builtin_amdgcn_update_dpp
 // (ma,ea) + (mb,eb) -> normalized; zero results keep a (very negative) exponent >= XF_EZERO
 // instead of exactly XF_EZERO: the mantissa is the same as xf_add's and a zero's exponent stays
 // below every live exponent, so every value downstream is bit-identical.
+//
+// Lazy normalization (!OBS, NORM false): the sum is left unnormalized, (s, em), and only every
+// kChainNorm-th step pays frexp. Every operation a row then meets -- f32 products and sums of
+// ldexp-aligned terms, in the chain, in the gradient products and in the Z tree -- is exact
+// under a power-of-two rescaling of its operands, and the mantissas stay within [2^-8, 2^8]
+// between normalizations (factor mantissas lie in [0.707, 1.414], all terms are >= 0), far from
+// f32 overflow and from the subnormal range wherever a term can still affect a rounded sum. So
+// the value represented is the oracle's to the bit, whatever the step's normalization; only
+// xf_log needs a normalized input (the debug rows normalize first). The zero clamp moves into
+// the exponent max (v_max3_i32) and is therefore applied on every step.
+constexpr int kChainNorm = 4;
+template <bool NORM>
 __device__ __forceinline__ void chain_add(float ma, int ea, float mb, int eb, float om, int oe,
                                           bool obs, float& m, int& e) {
-  const int em = max(ea, eb);
-  float s = xldexp(ma, ea - em) + xldexp(mb, eb - em);
-  int ee = em;
   if (obs) {
+    const int em = max(ea, eb);
+    float s = xldexp(ma, ea - em) + xldexp(mb, eb - em);
     s = s * om;
-    ee = ee + oe;
+    const int ee = em + oe;
+    m = xmant(s);
+    e = max(ee + xexpo(s), XF_EZERO);
+    return;
   }
-  m = xmant(s);
-  e = max(ee + xexpo(s), XF_EZERO);
+  const int em = max(max(ea, eb), XF_EZERO);
+  const float s = xldexp(ma, ea - em) + xldexp(mb, eb - em);
+  if constexpr (NORM) {
+    m = xmant(s);
+    e = em + xexpo(s);
+  } else {
+    m = s;
+    e = em;
+  }
 }
 
 // alpha[s+1] = (alpha[s] * E + alpha[s][p-1] * Sh[p-1]) (* O); L = pre-shifted shift factors
-template <int K, bool OBS>
+template <int K, bool OBS, bool NORM>
 __device__ __forceinline__ void alpha_chain(XRow<K>& A, const XRow<K>& E, const XRow<K>& L,
                                             const XRow<K>& O) {
   float hm[K];
@@ -244,11 +278,11 @@ __device__ __forceinline__ void alpha_chain(XRow<K>& A, const XRow<K>& E, const 
   }
 #pragma unroll
   for (int j = 0; j < K; ++j)
-    chain_add(A.m[j] * E.m[j], A.e[j] + E.e[j], hm[j], he[j], O.m[j], O.e[j], OBS, A.m[j], A.e[j]);
+    chain_add<NORM>(A.m[j] * E.m[j], A.e[j] + E.e[j], hm[j], he[j], O.m[j], O.e[j], OBS, A.m[j], A.e[j]);
 }
 
 // beta[s] = E * Q[p] + Sh * Q[p+1], Q = beta[s+1] (* O[s+1])
-template <int K, bool OBS>
+template <int K, bool OBS, bool NORM>
 __device__ __forceinline__ void beta_chain(XRow<K>& Bt, const XRow<K>& E, const XRow<K>& Sh,
                                            const XRow<K>& O) {
   float qm[K];
@@ -267,7 +301,7 @@ __device__ __forceinline__ void beta_chain(XRow<K>& Bt, const XRow<K>& E, const 
   }
 #pragma unroll
   for (int j = 0; j < K; ++j)
-    chain_add(E.m[j] * qm[j], E.e[j] + qe[j], rm[j], re[j], 0.0f, 0, false, Bt.m[j], Bt.e[j]);
+    chain_add<OBS || NORM>(E.m[j] * qm[j], E.e[j] + qe[j], rm[j], re[j], 0.0f, 0, false, Bt.m[j], Bt.e[j]);
 }
 
 template <int K>
@@ -576,8 +610,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
             float va[K], vb[K];
 #pragma unroll
             for (int q = 0; q < K; ++q) {
-              va[q] = zero_z ? -__builtin_inff() : xf_log(xf{A.m[q], A.e[q]});
-              vb[q] = zero_z ? -__builtin_inff() : xf_log(xf{Bs.m[q], Bs.e[q]});
+              va[q] = zero_z ? -__builtin_inff() : xf_log(xf_norm(A.m[q], A.e[q]));  // (lazy rows)
+              vb[q] = zero_z ? -__builtin_inff() : xf_log(xf_norm(Bs.m[q], Bs.e[q]));
             }
             if (la) buf_st<K>(va, brsrc(la + (size_t)s * U, U * 4u), p0 * 4);
             if (lb) buf_st<K>(vb, brsrc(lb + (size_t)s * U, U * 4u), p0 * 4);
@@ -611,6 +645,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     const int d = role.d;
     const int c = role.idx;
     constexpr int D = conv_depth<K>();
+    if (SSNT_T_CPRIO > 0) __builtin_amdgcn_s_setprio(SSNT_T_CPRIO);
     const unsigned tag0 = (d == 0 && c == 0 && b == 0 && a.loss_sum) ? sum_tag(a) : 0u;
     const int chain_end = d == 0 ? S - 1 : S;
     unsigned char* ring = inr + (size_t)d * R * slot_bytes;
@@ -821,7 +856,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       constexpr bool phase2 = decltype(Ph)::value;
       if (!live) return;
       const int r = base + i;
-      alpha_chain<K, OBS>(X, Eb[par], Xb[par], Ob[par]);
+      alpha_chain<K, OBS, (i % kChainNorm) == kChainNorm - 1>(X, Eb[par], Xb[par], Ob[par]);
       if constexpr (!phase2) {
         if constexpr (LDS) {
           if (!EXP(5)) lds_xrow_st<K>(wp, X);
@@ -902,7 +937,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       constexpr int par = i % PF;
       if (!live) return;
       const int r = base + i;
-      beta_chain<K, OBS>(X, Eb[par], Xb[par], Ob[par]);
+      beta_chain<K, OBS, (i % kChainNorm) == kChainNorm - 1>(X, Eb[par], Xb[par], Ob[par]);
       put(r, i, Kd);
       rd((i + PF) % R, Eb[par], Xb[par], Ob[par]);
     };
@@ -960,7 +995,7 @@ int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
   return launch_stream_k<2, false, 3, 4>(a, st);
 #else
   if (a.U <= 64) return launch_stream_k<1, OBS, 3, 4>(a, st);
-  if (a.U <= 128) return launch_stream_k<2, OBS, 3, 4>(a, st);
+  if (a.U <= 128) return launch_stream_k<2, OBS, SSNT_T_NC, SSNT_T_NH>(a, st);
   if (a.U <= 256) return launch_stream_k<4, OBS, 2, 2>(a, st);
   // K = 8 (U <= 512, configs[4]): the two-wave kernel. The streaming kernel needs 4-slot rings to
   // fit LDS there and then ran 2.2x slower (5.7 vs 2.6 ms at B=64 T=2000 U=400).
