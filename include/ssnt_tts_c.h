@@ -153,6 +153,25 @@ int ssnt_fwd_bwd(const float *log_trans, const float *log_obs, const int *step_l
                  float *loss, float *grad_trans, float *grad_obs, float *log_alpha,
                  float *log_beta);
 
+/* ---- F4: v2 duration-class (semi-Markov) forward-backward (DESIGN.md
+ * "Duration lattice"). New: the reference only decodes this lattice; the move rules are the v2
+ * decode's (src/v2.rs:94-166 -- band, overrun, exact final total, zero-duration class; test_mode
+ * keeps only the class rule). logits (B,T,D) per-step class log-probs (teacher-forced, one row
+ * per input step); duration_table (D) >= 0; input_length I_b <= T, output_length O_b (B).
+ * State totals run 0..max_total (totals above it -- test mode only -- are outside the lattice).
+ * Outputs: loss (B) = -ln Z, Z = sum over every admissible class sequence of its probability
+ * (+inf when none, 0 with SSNT_FLAG_ZERO_INFINITY); grad (B,T,D) = d loss / d logits = minus
+ * the class posteriors (NULL = skip); log_alpha / log_beta (B,T+1,max_total+1) debug rows
+ * (NULL = skip). `workspace` holds ssnt_v2_fwd_bwd_workspace_size() bytes. Device pointers,
+ * asynchronous on `stream`; a negative duration sets SSNT_ERR_BAD_INDEX in `status`. */
+size_t ssnt_v2_fwd_bwd_workspace_size(int batch, int max_steps, int max_total, bool test_mode);
+int ssnt_v2_fwd_bwd_device(const float *logits, const int *duration_table, const int *input_length,
+                           const int *output_length, int batch, int max_steps,
+                           int duration_class_size, int max_total, int zero_duration_id,
+                           bool allow_skip, bool test_mode, int flags, float *loss, float *grad,
+                           float *log_alpha, float *log_beta, void *workspace,
+                           size_t workspace_bytes, int *status, void *stream);
+
 /* ---- batched decode steps, device pointers (the reference FFI fixes v1 to B=1,
  * ssnt_tts_c/src/lib.rs:13; its Rust API takes B, src/lib.rs:121). max_beam_width = beam_width
  * as in every reference call site (ssnt_tts_c/src/lib.rs:82,217,342). ---- */

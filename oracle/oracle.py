@@ -347,3 +347,53 @@ def synth_tone_logits(B, T, W, C, seed=0, tie_rich=False):
     z = rng.standard_normal((B, T, W, C)).astype(np.float32) * np.float32(1.5)
     m = z.max(axis=-1, keepdims=True)
     return (z - (m + np.log(np.exp(z - m).sum(axis=-1, keepdims=True)))).astype(np.float32)
+
+
+def v2_fwd_bwd(logits, duration_table, input_length, output_length, max_total, zero_duration_id,
+               allow_skip, test_mode, flags=0, debug=False, n_threads=0):
+    """F4: v2 duration-class fwd-bwd, exact split-exponent arithmetic (the bits the HIP kernel
+    reproduces). logits (B,I,D). Returns dict(loss, grad[, log_alpha, log_beta])."""
+    lg = _f32(logits)
+    B, I, D = lg.shape
+    X = int(max_total) + 1
+    loss = np.zeros(B, np.float32)
+    grad = np.zeros((B, I, D), np.float32)
+    la = np.zeros((B, I + 1, X), np.float32) if debug else None
+    lb = np.zeros((B, I + 1, X), np.float32) if debug else None
+    rc = lib().oracle_v2_fwd_bwd(
+        B, I, D, int(max_total), _p(lg, _f32p), _p(_i32(duration_table), _i32p),
+        _p(_i32(input_length), _i32p), _p(_i32(output_length), _i32p), int(zero_duration_id),
+        ctypes.c_bool(allow_skip), ctypes.c_bool(test_mode), int(flags), _p(loss, _f32p),
+        _p(grad, _f32p), _p(la, _f32p), _p(lb, _f32p), int(n_threads))
+    if rc != 0:
+        raise RuntimeError(f"oracle_v2_fwd_bwd status {rc}")
+    out = dict(loss=loss, grad=grad)
+    if debug:
+        out["log_alpha"] = la
+        out["log_beta"] = lb
+    return out
+
+
+def v2_fwd_bwd_f64(logits, duration_table, input_length, output_length, max_total,
+                   zero_duration_id, allow_skip, test_mode):
+    """F4 float64 log-domain definition (rules applied per move, no windows)."""
+    lg = _f32(logits)
+    B, I, D = lg.shape
+    loss = np.zeros(B, np.float64)
+    grad = np.zeros((B, I, D), np.float64)
+    lib().oracle_v2_fwd_bwd_f64(
+        B, I, D, int(max_total), _p(lg, _f32p), _p(_i32(duration_table), _i32p),
+        _p(_i32(input_length), _i32p), _p(_i32(output_length), _i32p), int(zero_duration_id),
+        ctypes.c_bool(allow_skip), ctypes.c_bool(test_mode), _p(loss, _f64p), _p(grad, _f64p))
+    return dict(loss=loss, grad=grad)
+
+
+def synth_v2_step_logits(durations, D, seed=0, margin=3.0):
+    """Teacher-forced per-step class logits (B,I,D) for the F4 fwd-bwd: log_softmax of N(0,1)
+    plus `margin` at each step's sampled duration class (duration_table = [0..D-1])."""
+    rng = np.random.default_rng(seed)
+    B, T = durations.shape
+    z = rng.standard_normal((B, T, D)).astype(np.float32)
+    z += np.float32(margin) * np.eye(D, dtype=np.float32)[durations]
+    m = z.max(axis=-1, keepdims=True)
+    return (z - (m + np.log(np.exp(z - m).sum(axis=-1, keepdims=True)))).astype(np.float32)

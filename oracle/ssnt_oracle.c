@@ -918,3 +918,280 @@ int oracle_omp_max_threads(void) {
     return 1;
 #endif
 }
+
+/* ==========================================================================================
+ * F4: v2 duration-class forward-backward (DESIGN.md "Duration lattice").
+ *
+ * Not in the reference: the training-side counterpart of the v2 decode's expansion rules
+ * (src/v2.rs:94-166). State (r, x): r = input steps consumed (0..I), x = total duration so far
+ * (0..X-1, X = max_total + 1). Step t (row t -> t+1) picks one class i with weight
+ * exp(logits[t][i]) and adds duration_table[i]; the move exists iff decode_beam_at would keep
+ * that candidate (src/v2.rs:127-164):
+ *   class rule, always:  !allow_skip && i == zero_duration_id is dropped (src/v2.rs:139,152);
+ *   unless test_mode:    the new total inside total_duration_bounds(t) (src/v2.rs:94-104,131),
+ *                        !will_overrun(t) (src/v2.rs:106-111,133),
+ *                        at t = I-1 the new total == O (src/v2.rs:135-137).
+ * Totals above max_total are outside the state space (reachable in test mode only).
+ * Z = sum_x alpha[I][x]; loss = -ln Z (Z == 0: +inf, 0 with FLAG_ZERO_INFINITY, grads 0);
+ * grad[t][i] = d loss / d logits[t][i] = -(posterior of class i at step t).
+ *
+ * Arithmetic (what csrc/v2_fwd_bwd.hip reproduces bit for bit): split-exponent xf as in the
+ * lattice above; w[t][i] = xf_exp(logits[t][i], class rule);
+ *   cell sums over classes (alpha, beta): terms in class order i = 0..D-1, em = max_i e_i,
+ *     s = sum_i ldexp(m_i, e_i - em) accumulated in class order, then xf_norm(s, em);
+ *   sums over totals (Z, gradients): 64 partial sums -- total x goes to partial x mod 64, each
+ *     accumulated with xf_add in increasing x -- then an xor butterfly over offsets 1..32 with
+ *     xf_add (commutative: every partial ends equal).
+ * Rows are only evaluated inside their window (f4_window): cells outside are exact zeros, and
+ * neither sum depends on which zero cells it skips.
+ * ========================================================================================== */
+typedef struct {
+    int I, O, X, D, dmax, zid;
+    bool allow_skip, test_mode;
+    const int32_t *dur;
+} f4_ctx;
+
+/* cells of row r that can be nonzero: [*lo, *hi] (empty when *lo > *hi) */
+static void f4_window(const f4_ctx *c, int r, int *lo, int *hi) {
+    if (r == 0) { *lo = 0; *hi = 0; return; }
+    if (c->test_mode) {
+        const long long h = (long long)r * c->dmax;
+        *lo = 0;
+        *hi = h < c->X - 1 ? (int)h : c->X - 1;
+        return;
+    }
+    const int t = r - 1;
+    if ((long long)(c->I - (t + 1)) * 3 > c->O) { *lo = 1; *hi = 0; return; } /* src/v2.rs:106-111 */
+    const float diagonal = (float)c->O / (float)c->I * (float)(t + 1);      /* src/v2.rs:94-104 */
+    const float upper_range = (float)c->O * 0.1f;
+    const float lower_range = (float)c->O * 0.05f;
+    int lb = f2i_sat(fmaxf(diagonal - lower_range, 0.0f));
+    int ub = f2i_sat(fminf(diagonal + upper_range, (float)c->O));
+    if (t == c->I - 1) { /* src/v2.rs:135-137 */
+        lb = lb > c->O ? lb : c->O;
+        ub = ub < c->O ? ub : c->O;
+    }
+    *lo = lb > 0 ? lb : 0;
+    *hi = ub < c->X - 1 ? ub : c->X - 1;
+}
+
+static inline bool f4_in(int x, int lo, int hi) { return x >= lo && x <= hi; }
+
+/* class-order cell sum of D terms */
+static xf f4_cell_sum(const xf *term, int D) {
+    int32_t em = term[0].e;
+    for (int i = 1; i < D; ++i) em = term[i].e > em ? term[i].e : em;
+    float s = 0.0f;
+    for (int i = 0; i < D; ++i) s = s + ldexpf(term[i].m, term[i].e - em);
+    return xf_norm(s, em);
+}
+
+/* 64 partials (x mod 64, increasing x) + xor butterfly: acc[64] in, result out */
+static xf f4_butterfly(xf *acc) {
+    xf nxt[64];
+    for (int off = 1; off < 64; off <<= 1) {
+        for (int l = 0; l < 64; ++l) nxt[l] = xf_add(acc[l].m, acc[l].e, acc[l ^ off].m, acc[l ^ off].e);
+        memcpy(acc, nxt, sizeof(nxt));
+    }
+    return acc[0];
+}
+
+static void f4_one(const f4_ctx *c, int Imax, const float *lg, float *loss, float *g,
+                   float *la, float *lb, int flags, xf *A, xf *Bt, xf *w, xf *term) {
+    const int X = c->X, D = c->D, I = c->I;
+    const float inf_loss = (flags & FLAG_ZERO_INFINITY) ? 0.0f : INFINITY;
+    if (g) memset(g, 0, sizeof(float) * (size_t)Imax * D);
+    for (size_t k = 0; la && k < (size_t)(Imax + 1) * X; ++k) la[k] = -INFINITY;
+    for (size_t k = 0; lb && k < (size_t)(Imax + 1) * X; ++k) lb[k] = -INFINITY;
+    if (I <= 0 || I > Imax || c->O < 0) { *loss = inf_loss; return; }
+    for (int t = 0; t < I; ++t)
+        for (int i = 0; i < D; ++i)
+            w[(size_t)t * D + i] = xf_exp(lg[(size_t)t * D + i], c->allow_skip || i != c->zid);
+    const xf zero = {0.0f, XF_EZERO};
+    /* alpha */
+    for (size_t k = 0; k < (size_t)(I + 1) * X; ++k) A[k] = zero;
+    A[0] = (xf){0.5f, 1};
+    for (int r = 1; r <= I; ++r) {
+        int plo, phi, lo, hi;
+        f4_window(c, r - 1, &plo, &phi);
+        f4_window(c, r, &lo, &hi);
+        for (int x = lo; x <= hi; ++x) {
+            for (int i = 0; i < D; ++i) {
+                const int y = x - c->dur[i];
+                if (f4_in(y, plo, phi)) {
+                    const xf a = A[(size_t)(r - 1) * X + y], ww = w[(size_t)(r - 1) * D + i];
+                    term[i] = (xf){a.m * ww.m, a.e + ww.e};
+                } else {
+                    term[i] = zero;
+                }
+            }
+            A[(size_t)r * X + x] = f4_cell_sum(term, D);
+        }
+    }
+    for (int r = 0; la && r <= I; ++r) {
+        int lo, hi;
+        f4_window(c, r, &lo, &hi);
+        for (int x = lo; x <= hi; ++x) la[(size_t)r * X + x] = xf_log(A[(size_t)r * X + x]);
+    }
+    /* Z */
+    xf acc[64];
+    for (int l = 0; l < 64; ++l) acc[l] = zero;
+    {
+        int lo, hi;
+        f4_window(c, I, &lo, &hi);
+        for (int x = lo; x <= hi; ++x) {
+            const xf a = A[(size_t)I * X + x];
+            acc[x & 63] = xf_add(acc[x & 63].m, acc[x & 63].e, a.m, a.e);
+        }
+    }
+    const xf Z = f4_butterfly(acc);
+    if (Z.m == 0.0f) { *loss = inf_loss; return; }
+    *loss = 0.0f - xf_log(Z);
+    const float izm = 1.0f / Z.m;
+    const int32_t ize = -Z.e;
+    /* beta */
+    for (size_t k = 0; k < (size_t)(I + 1) * X; ++k) Bt[k] = zero;
+    {
+        int lo, hi;
+        f4_window(c, I, &lo, &hi);
+        for (int x = lo; x <= hi; ++x) Bt[(size_t)I * X + x] = (xf){0.5f, 1};
+    }
+    for (int r = I - 1; r >= 0; --r) {
+        int lo, hi, nlo, nhi;
+        f4_window(c, r, &lo, &hi);
+        f4_window(c, r + 1, &nlo, &nhi);
+        for (int y = lo; y <= hi; ++y) {
+            for (int i = 0; i < D; ++i) {
+                const int x = y + c->dur[i];
+                if (f4_in(x, nlo, nhi)) {
+                    const xf bb = Bt[(size_t)(r + 1) * X + x], ww = w[(size_t)r * D + i];
+                    term[i] = (xf){ww.m * bb.m, ww.e + bb.e};
+                } else {
+                    term[i] = zero;
+                }
+            }
+            Bt[(size_t)r * X + y] = f4_cell_sum(term, D);
+        }
+    }
+    for (int r = 0; lb && r <= I; ++r) {
+        int lo, hi;
+        f4_window(c, r, &lo, &hi);
+        for (int x = lo; x <= hi; ++x) lb[(size_t)r * X + x] = xf_log(Bt[(size_t)r * X + x]);
+    }
+    /* gradients: posterior of class i at step t over the moves into row t+1 */
+    for (int t = 0; g && t < I; ++t) {
+        int plo, phi, lo, hi;
+        f4_window(c, t, &plo, &phi);
+        f4_window(c, t + 1, &lo, &hi);
+        for (int i = 0; i < D; ++i) {
+            for (int l = 0; l < 64; ++l) acc[l] = zero;
+            for (int x = lo; x <= hi; ++x) {
+                const int y = x - c->dur[i];
+                if (!f4_in(y, plo, phi)) continue;
+                const xf a = A[(size_t)t * X + y], bb = Bt[(size_t)(t + 1) * X + x];
+                acc[x & 63] = xf_add(acc[x & 63].m, acc[x & 63].e, a.m * bb.m, a.e + bb.e);
+            }
+            const xf S = f4_butterfly(acc);
+            const xf ww = w[(size_t)t * D + i];
+            g[(size_t)t * D + i] = xf_neg_post((S.m * ww.m) * izm, S.e + ww.e + ize);
+        }
+    }
+}
+
+/* logits (B, Imax, D); duration_table (D) >= 0; input_length / output_length (B); X = max_total+1.
+ * Outputs: loss (B); grad (B, Imax, D) or NULL; log_alpha / log_beta (B, Imax+1, X) or NULL. */
+int oracle_v2_fwd_bwd(int B, int Imax, int D, int max_total, const float *logits,
+                      const int32_t *duration_table, const int32_t *input_length,
+                      const int32_t *output_length, int zero_duration_id, bool allow_skip,
+                      bool test_mode, int flags, float *loss, float *grad, float *log_alpha,
+                      float *log_beta, int n_threads) {
+    if (B < 0 || Imax <= 0 || D <= 0 || max_total < 0) return ORC_ERR_INVALID;
+    int dmax = 0;
+    for (int i = 0; i < D; ++i) {
+        if (duration_table[i] < 0) return ORC_ERR_INVALID;
+        dmax = duration_table[i] > dmax ? duration_table[i] : dmax;
+    }
+    const int X = max_total + 1;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel
+#endif
+    {
+        xf *A = (xf *)malloc(sizeof(xf) * (size_t)(Imax + 1) * X);
+        xf *Bt = (xf *)malloc(sizeof(xf) * (size_t)(Imax + 1) * X);
+        xf *w = (xf *)malloc(sizeof(xf) * (size_t)Imax * D);
+        xf *term = (xf *)malloc(sizeof(xf) * (size_t)D);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic)
+#endif
+        for (int b = 0; b < B; ++b) {
+            f4_ctx c = {input_length[b], output_length[b], X, D, dmax, zero_duration_id,
+                        allow_skip, test_mode, duration_table};
+            const size_t rows = (size_t)(Imax + 1) * X;
+            f4_one(&c, Imax, logits + (size_t)b * Imax * D, loss + b,
+                   grad ? grad + (size_t)b * Imax * D : NULL, log_alpha ? log_alpha + b * rows : NULL,
+                   log_beta ? log_beta + b * rows : NULL, flags, A, Bt, w, term);
+        }
+        free(A);
+        free(Bt);
+        free(w);
+        free(term);
+    }
+    return ORC_OK;
+}
+
+/* Independent float64 log-domain definition of the same lattice (no windows: every state,
+ * the rules applied per move), for pinning the xf arithmetic. loss (B), grad (B, Imax, D). */
+int oracle_v2_fwd_bwd_f64(int B, int Imax, int D, int max_total, const float *logits,
+                          const int32_t *duration_table, const int32_t *input_length,
+                          const int32_t *output_length, int zero_duration_id, bool allow_skip,
+                          bool test_mode, double *loss, double *grad) {
+    const int X = max_total + 1;
+    double *A = (double *)malloc(sizeof(double) * (size_t)(Imax + 1) * X);
+    double *Bt = (double *)malloc(sizeof(double) * (size_t)(Imax + 1) * X);
+    for (int b = 0; b < B; ++b) {
+        const int I = input_length[b], O = output_length[b];
+        const float *lg = logits + (size_t)b * Imax * D;
+        double *g = grad + (size_t)b * Imax * D;
+        for (int k = 0; k < Imax * D; ++k) g[k] = 0.0;
+        if (I <= 0 || I > Imax) { loss[b] = INFINITY; continue; }
+        v2_ctx vc = {(uint64_t)I, (uint64_t)O, NULL, duration_table, D, zero_duration_id, allow_skip, test_mode};
+        /* move (t, x -> x + d_i) allowed? */
+#define F4_OK(t, nx, i)                                                                          \
+    ((allow_skip || (i) != zero_duration_id) && (nx) >= 0 && (nx) < X &&                         \
+     (test_mode || (({ int32_t lb_, ub_; v2_bounds(&vc, (uint64_t)(t), &lb_, &ub_);               \
+                       (nx) >= lb_ && (nx) <= ub_; }) && !v2_will_overrun(&vc, (uint64_t)(t)) &&  \
+                    ((t) != I - 1 || (nx) == O))))
+        for (size_t k = 0; k < (size_t)(I + 1) * X; ++k) A[k] = Bt[k] = -INFINITY;
+        A[0] = 0.0;
+        for (int t = 0; t < I; ++t)
+            for (int x = 0; x < X; ++x) {
+                if (A[(size_t)t * X + x] == -INFINITY) continue;
+                for (int i = 0; i < D; ++i) {
+                    const int nx = x + duration_table[i];
+                    if (!F4_OK(t, nx, i) || !(lg[(size_t)t * D + i] >= XF_LOG_MIN)) continue;
+                    double *dst = &A[(size_t)(t + 1) * X + nx];
+                    *dst = lse2(*dst, A[(size_t)t * X + x] + (double)lg[(size_t)t * D + i]);
+                }
+            }
+        double Z = -INFINITY;
+        for (int x = 0; x < X; ++x) Z = lse2(Z, A[(size_t)I * X + x]);
+        if (Z == -INFINITY) { loss[b] = INFINITY; continue; }
+        loss[b] = -Z;
+        for (int x = 0; x < X; ++x) Bt[(size_t)I * X + x] = 0.0;
+        for (int t = I - 1; t >= 0; --t)
+            for (int x = 0; x < X; ++x)
+                for (int i = 0; i < D; ++i) {
+                    const int nx = x + duration_table[i];
+                    if (!F4_OK(t, nx, i) || !(lg[(size_t)t * D + i] >= XF_LOG_MIN)) continue;
+                    const double v = (double)lg[(size_t)t * D + i] + Bt[(size_t)(t + 1) * X + nx];
+                    Bt[(size_t)t * X + x] = lse2(Bt[(size_t)t * X + x], v);
+                    const double post = A[(size_t)t * X + x] + v - Z;
+                    g[(size_t)t * D + i] -= exp(post);
+                }
+#undef F4_OK
+    }
+    free(A);
+    free(Bt);
+    return ORC_OK;
+}

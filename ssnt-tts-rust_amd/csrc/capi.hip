@@ -539,6 +539,27 @@ int ssnt_fwd_bwd_sum_device(const float* log_trans, const float* log_obs, const 
   return launch_fwd_bwd(a, as_stream(stream));
 }
 
+size_t ssnt_v2_fwd_bwd_workspace_size(int batch, int max_steps, int max_total, bool test_mode) {
+  return v2_fwd_bwd_workspace_bytes(batch, max_steps, max_total, test_mode);
+}
+
+int ssnt_v2_fwd_bwd_device(const float* logits, const int* duration_table, const int* input_length,
+                           const int* output_length, int batch, int max_steps,
+                           int duration_class_size, int max_total, int zero_duration_id,
+                           bool allow_skip, bool test_mode, int flags, float* loss, float* grad,
+                           float* log_alpha, float* log_beta, void* workspace,
+                           size_t workspace_bytes, int* status, void* stream) {
+  if (max_total < 0 || max_total > (1 << 24)) return SSNT_ERR_INVALID_ARG;
+  V2FwdBwdArgs a{};
+  a.logits = logits; a.table = duration_table; a.input_length = input_length;
+  a.output_length = output_length; a.B = batch; a.Imax = max_steps; a.D = duration_class_size;
+  a.X = max_total + 1; a.zid = zero_duration_id; a.allow_skip = allow_skip;
+  a.test_mode = test_mode; a.flags = flags; a.loss = loss; a.grad = grad;
+  a.log_alpha = log_alpha; a.log_beta = log_beta; a.workspace = workspace;
+  a.workspace_bytes = workspace_bytes; a.status = status;
+  return launch_v2_fwd_bwd(a, as_stream(stream));
+}
+
 int ssnt_fwd_bwd(const float* log_trans, const float* log_obs, const int* step_len,
                  const int* pos_len, int batch, int max_steps, int max_pos, int flags,
                  float* loss, float* grad_trans, float* grad_obs, float* log_alpha,

@@ -52,6 +52,29 @@ int set_fwd_bwd_wide_lanes(int k);  // A/B: positions per lane of the long-row k
 size_t stream_head_bytes(int K, int U, bool obs, int ring = 0);  // LDS bytes besides the lattice rows
 int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only (tools/diag_fwd_bwd.py)
 
+// ---- F4: v2 duration-class forward-backward (v2_fwd_bwd.hip) ----
+struct V2FwdBwdArgs {
+  const float* logits;       // (B, Imax, D) per-step class log-probs
+  const int* table;          // (D) duration_table, >= 0
+  const int* input_length;   // (B) I_b <= Imax
+  const int* output_length;  // (B) O_b
+  int B, Imax, D, X;         // X = max_total + 1 totals per row
+  int zid;                   // zero_duration_id
+  bool allow_skip, test_mode;
+  int flags;                 // SSNT_FLAG_ZERO_INFINITY
+  float* loss;               // (B)
+  float* grad;               // (B, Imax, D) or null
+  float* log_alpha;          // (B, Imax+1, X) or null
+  float* log_beta;           // (B, Imax+1, X) or null
+  void* workspace;
+  size_t workspace_bytes;
+  int Wcap;                  // set by the launcher
+  int* status;
+};
+size_t v2_fwd_bwd_wcap(int max_total, bool test_mode);
+size_t v2_fwd_bwd_workspace_bytes(int B, int Imax, int max_total, bool test_mode);
+int launch_v2_fwd_bwd(const V2FwdBwdArgs& a, hipStream_t stream);
+
 // ---- beam-search decode (decode.hip) ----
 enum class Variant : int { V1 = 0, V2 = 1, Tone = 2 };
 

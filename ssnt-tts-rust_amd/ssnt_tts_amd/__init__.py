@@ -27,7 +27,8 @@ __all__ = [
     "order_beam_branch", "upsample_source_indexes", "tone_latent_beam_search_decode",
     "levenshtein_edit_distance", "ssnt_fwd_bwd", "SSNTLatticeLoss", "ssnt_lattice_loss",
     "lattice_beam_search_decode", "v2_lattice_beam_search_decode",
-    "tone_latent_lattice_beam_search_decode", "SsntError", "FLAG_TERMINAL_EMIT", "FLAG_ZERO_INFINITY",
+    "tone_latent_lattice_beam_search_decode", "v2_fwd_bwd", "V2DurationLoss", "v2_duration_loss",
+    "SsntError", "FLAG_TERMINAL_EMIT", "FLAG_ZERO_INFINITY",
 ]
 
 
@@ -367,6 +368,82 @@ def ssnt_lattice_loss(log_trans, step_len, pos_len, log_obs=None, terminal_emit=
                       zero_infinity=False, check=True):
     return SSNTLatticeLoss.apply(log_trans, step_len, pos_len, log_obs, terminal_emit,
                                  zero_infinity, check)
+
+
+# ----------------------------------------------------------------------------------------------
+# F4: v2 duration-class forward-backward (DESIGN.md "Duration lattice")
+# ----------------------------------------------------------------------------------------------
+def v2_fwd_bwd(logits, duration_table, input_length, output_length, zero_duration_id, *,
+               allow_skip=False, test_mode=False, max_total=None, zero_infinity=False,
+               need_grad=True, debug=False, check=False):
+    """Forward-backward over the v2 duration-class lattice: the sum over every class sequence the
+    v2 decode could keep (src/v2.rs:94-166 move rules) of its probability.
+
+    logits (B,T,D) per-step class log-probs (teacher-forced); duration_table (D,) >= 0;
+    input_length / output_length (B,). ``max_total`` bounds the state totals (default
+    max(output_length), read back from the device). Returns ``loss`` (B,) = -ln Z, ``grad``
+    (B,T,D) = d loss / d logits (= minus the class posteriors), and with ``debug`` the rows
+    ``log_alpha`` / ``log_beta`` (B,T+1,max_total+1)."""
+    lib = load(require_gpu=True)
+    lg = _dev(logits, torch.float32, "logits")
+    dev = lg.device
+    B, T, D = lg.shape
+    table = _dev(duration_table, torch.int32, "duration_table").reshape(D)
+    il = _dev(input_length, torch.int32, "input_length").reshape(B)
+    ol = _dev(output_length, torch.int32, "output_length").reshape(B)
+    if max_total is None:
+        max_total = int(ol.max().item()) if B > 0 else 0
+    X = int(max_total) + 1
+    loss = torch.empty(B, dtype=torch.float32, device=dev)
+    grad = torch.empty((B, T, D), dtype=torch.float32, device=dev) if need_grad else None
+    la = torch.empty((B, T + 1, X), dtype=torch.float32, device=dev) if debug else None
+    lb = torch.empty((B, T + 1, X), dtype=torch.float32, device=dev) if debug else None
+    wsb = int(lib.ssnt_v2_fwd_bwd_workspace_size(B, T, int(max_total), bool(test_mode)))
+    ws = _workspace(dev, wsb)
+    st = _status(dev)
+    rc = lib.ssnt_v2_fwd_bwd_device(_p(lg), _p(table), _p(il), _p(ol), B, T, D, int(max_total),
+                                    int(zero_duration_id), bool(allow_skip), bool(test_mode),
+                                    FLAG_ZERO_INFINITY if zero_infinity else 0, _p(loss),
+                                    _p(grad), _p(la), _p(lb), _p(ws), wsb, _p(st), _stream(dev))
+    _finish("v2_fwd_bwd", rc, st, check)
+    res = {"loss": loss, "status": st}
+    if grad is not None:
+        res["grad"] = grad
+    if debug:
+        res["log_alpha"] = la
+        res["log_beta"] = lb
+    return res
+
+
+class V2DurationLoss(torch.autograd.Function):
+    """Autograd wrapper of v2_fwd_bwd: per-utterance loss (B,), gradients from the same launch."""
+
+    @staticmethod
+    def forward(ctx, logits, duration_table, input_length, output_length, zero_duration_id,
+                allow_skip=False, test_mode=False, max_total=None, zero_infinity=False, check=True):
+        r = v2_fwd_bwd(logits.detach(), duration_table, input_length, output_length,
+                       zero_duration_id, allow_skip=allow_skip, test_mode=test_mode,
+                       max_total=max_total, zero_infinity=zero_infinity,
+                       need_grad=logits.requires_grad)
+        ctx.save_for_backward(r.get("grad"), r["status"])
+        ctx.check = check
+        return r["loss"]
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        g, st = ctx.saved_tensors
+        if ctx.check:
+            _finish("v2_duration_loss", 0, st, True)
+        gl = None if g is None else g * grad_loss.to(torch.float32)[:, None, None]
+        return gl, None, None, None, None, None, None, None, None, None
+
+
+def v2_duration_loss(logits, duration_table, input_length, output_length, zero_duration_id,
+                     allow_skip=False, test_mode=False, max_total=None, zero_infinity=False,
+                     check=True):
+    return V2DurationLoss.apply(logits, duration_table, input_length, output_length,
+                                zero_duration_id, allow_skip, test_mode, max_total, zero_infinity,
+                                check)
 
 
 def lattice_beam_search_decode(lattice, input_length, beam_width, *, check=True):

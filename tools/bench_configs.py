@@ -124,10 +124,29 @@ def tone_decode_config(B, I, C, W, iters):
             "cpu_beam_steps_per_s": steps / tc, "cpu_threads": THREADS}
 
 
+def v2_fwd_bwd_config(B, I, Ototal, D, iters):
+    """F4 at the configs[4] v2 shape: duration-class fwd-bwd, loss + grad."""
+    d = O.synth_durations(B, I, Ototal, D, seed=0)
+    lg_np = O.synth_v2_step_logits(d, D, seed=1)
+    table_np = np.arange(D, dtype=np.int32)
+    il_np, ol_np = np.full(B, I, np.int32), np.full(B, Ototal, np.int32)
+    lg, table = torch.from_numpy(lg_np).to(DEV), torch.from_numpy(table_np).to(DEV)
+    il, ol = torch.from_numpy(il_np).to(DEV), torch.from_numpy(ol_np).to(DEV)
+    S.v2_fwd_bwd(lg, table, il, ol, 0, max_total=Ototal, check=True)
+    t = gpu_time(lambda: S.v2_fwd_bwd(lg, table, il, ol, 0, max_total=Ototal), iters)
+    tc = cpu_time(lambda: O.v2_fwd_bwd(lg_np, table_np, il_np, ol_np, Ototal, 0, False, False,
+                                       n_threads=THREADS))
+    return {"config": "configs[4] F4", "workload": f"v2 duration fwd-bwd B={B} I={I} O={Ototal} "
+            f"D={D} loss+grad", "gpu_us": t * 1e6, "utterances_per_s": B / t,
+            "cpu_utterances_per_s": B / tc, "cpu_threads": THREADS,
+            "note": "one workgroup per utterance, 2 x I dependent steps over the band"}
+
+
 if __name__ == "__main__":
     print(json.dumps(fwd_bwd_config("configs[0]", 1, 50, 20, iters=50, cpu_sample=1)), flush=True)
     print(json.dumps(decode_config(256, 200, 80, 4, iters=10)), flush=True)
     print(json.dumps(fwd_bwd_config("configs[4]", 64, 2000, 400, iters=3, cpu_sample=16)), flush=True)
     print(json.dumps(v2_decode_config(64, 400, 2000, 16, 4, iters=10)), flush=True)
     print(json.dumps(tone_decode_config(64, 400, 5, 4, iters=10)), flush=True)
+    print(json.dumps(v2_fwd_bwd_config(64, 400, 2000, 16, iters=10)), flush=True)
     print(json.dumps({"host": HOST}), flush=True)
