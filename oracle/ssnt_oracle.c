@@ -937,8 +937,9 @@ int oracle_omp_max_threads(void) {
  *
  * Arithmetic (what csrc/v2_fwd_bwd.hip reproduces bit for bit): split-exponent xf as in the
  * lattice above; w[t][i] = xf_exp(logits[t][i], class rule);
- *   cell sums over classes (alpha, beta): terms in class order i = 0..D-1, em = max_i e_i,
- *     s = sum_i ldexp(m_i, e_i - em) accumulated in class order, then xf_norm(s, em);
+ *   cell sums over classes (alpha, beta), D <= 64: em = max_i e_i (at least XF_EZERO),
+ *     s = pairwise-tree sum of ldexp(m_i, e_i - em) over the classes zero-padded to a power of
+ *     two, then xf_norm(s, em);
  *   sums over totals (Z, gradients): 64 partial sums -- total x goes to partial x mod 64, each
  *     accumulated with xf_add in increasing x -- then an xor butterfly over offsets 1..32 with
  *     xf_add (commutative: every partial ends equal).
@@ -977,13 +978,19 @@ static void f4_window(const f4_ctx *c, int r, int *lo, int *hi) {
 
 static inline bool f4_in(int x, int lo, int hi) { return x >= lo && x <= hi; }
 
-/* class-order cell sum of D terms */
+/* cell sum of D <= 64 class terms: em = max exponent (padding terms count as exact zeros
+ * (0, EZERO)), then the ldexp-aligned f32 terms summed by a pairwise tree over the next power
+ * of two (pairs (2i, 2i+1) first, zero padding) */
 static xf f4_cell_sum(const xf *term, int D) {
-    int32_t em = term[0].e;
-    for (int i = 1; i < D; ++i) em = term[i].e > em ? term[i].e : em;
-    float s = 0.0f;
-    for (int i = 0; i < D; ++i) s = s + ldexpf(term[i].m, term[i].e - em);
-    return xf_norm(s, em);
+    int P2 = 1;
+    while (P2 < D) P2 <<= 1;
+    int32_t em = XF_EZERO;
+    for (int i = 0; i < D; ++i) em = term[i].e > em ? term[i].e : em;
+    float v[64];
+    for (int i = 0; i < P2; ++i) v[i] = i < D ? ldexpf(term[i].m, term[i].e - em) : 0.0f;
+    for (int len = P2; len > 1; len >>= 1)
+        for (int i = 0; i < len / 2; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+    return xf_norm(v[0], em);
 }
 
 /* 64 partials (x mod 64, increasing x) + xor butterfly: acc[64] in, result out */
@@ -1105,7 +1112,7 @@ int oracle_v2_fwd_bwd(int B, int Imax, int D, int max_total, const float *logits
                       const int32_t *output_length, int zero_duration_id, bool allow_skip,
                       bool test_mode, int flags, float *loss, float *grad, float *log_alpha,
                       float *log_beta, int n_threads) {
-    if (B < 0 || Imax <= 0 || D <= 0 || max_total < 0) return ORC_ERR_INVALID;
+    if (B < 0 || Imax <= 0 || D <= 0 || D > 64 || max_total < 0) return ORC_ERR_INVALID;
     int dmax = 0;
     for (int i = 0; i < D; ++i) {
         if (duration_table[i] < 0) return ORC_ERR_INVALID;

@@ -69,6 +69,7 @@ struct V2FwdBwdArgs {
   void* workspace;
   size_t workspace_bytes;
   int Wcap;                  // set by the launcher
+  int chunk;                 // set by the launcher
   int* status;
 };
 size_t v2_fwd_bwd_wcap(int max_total, bool test_mode);

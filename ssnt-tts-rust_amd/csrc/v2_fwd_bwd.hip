@@ -5,21 +5,24 @@
 // oracle/ssnt_oracle.c ("F4") and DESIGN.md "Duration lattice"; this kernel reproduces that
 // definition bit for bit.
 //
-// Layout: one workgroup (256 threads, 4 waves) per utterance. State rows r = 0..I (input steps
-// consumed) over totals x; only the window of row r (f4_window: the v2 band, or [0, r*dmax] in
-// test mode) can hold mass, so rows are stored window-relative, Wcap xf wide:
-//   LDS:  duration table | class weights w[t] (2 steps, double-buffered) | alpha rows (2) |
-//         beta rows (2)                                    -- 32*Wcap + 20*D bytes
-//   HBM:  alpha rows 0..I of every utterance (workspace, B*(Imax+1)*Wcap xf), written by the
-//         forward sweep, read back one row per step by the backward sweep.
-// Forward: per step, each thread owns cells x = lo + tid (+256 ...) and sums its D class terms
-// (two passes: exponent max, then the ldexp-aligned f32 sum in class order); one barrier per
-// step; the next step's class weights are converted in the same step by the first D threads.
-// Backward: per step, beta of row t (as the forward), and the gradients of step t: class i on
-// wave i % 4, its sum over destination totals in 64 lane partials (x mod 64) + an xor butterfly
-// -- the oracle's summation order. HBM traffic per utterance: logits once per sweep, alpha rows
-// once each way, the gradients once: a few hundred KB, so the sweeps are latency-bound
-// (I dependent steps), not bandwidth-bound.
+// Layout. alpha does not depend on beta or the other way round, so the two sweeps run at the
+// same time: launch 1 has one workgroup (512 threads, 8 waves) per (utterance, direction).
+// State rows r = 0..I (input steps consumed) over totals x; only the window of row r
+// (f4_window: the v2 band, or [0, r*dmax] in test mode) can hold mass, so rows are stored
+// window-relative, Wcap xf wide:
+//   LDS:  duration table | class weights w[t] (2 steps) | 2 rows (ping-pong) | 2 chunks of
+//         staged class log-probs
+//   HBM:  alpha and beta rows 0..I of every utterance (workspace), Z per utterance.
+// A sweep step: each thread owns cells x = lo + tid (+512 ...) and sums its D class terms
+// (exponent max, then the ldexp-aligned f32 sum in class order; the class loop is unrolled for
+// D <= 64 with the durations in SGPRs); one barrier per step. Class log-probs are staged into
+// LDS a chunk of steps ahead (one global round trip per chunk) and converted one step before
+// use, so no global load sits on the I-step dependency chain. The forward workgroup also forms
+// Z (lane partials x mod 64 + butterfly) and the loss.
+// Launch 2 (one workgroup per (utterance, step)): the gradients of step t -- class i on wave
+// i % 4, every class of a wave accumulated in one pass over the destination totals (lane
+// partial x mod 64, the oracle's order), one butterfly per class (DPP quad/mirror moves, a
+// swizzle, one bpermute) -- and the debug beta row. Fully parallel (B * I workgroups).
 #include <hip/hip_runtime.h>
 
 #include "ssnt_internal.h"
@@ -28,8 +31,7 @@
 namespace ssnt {
 namespace {
 
-constexpr int kF4Threads = 256;
-constexpr int kF4Waves = kF4Threads / 64;
+constexpr int kF4Threads = 512;
 
 __device__ __forceinline__ int f4_f2i(float x) {  // Rust `f32 as i32` (saturating, NaN -> 0)
   if (x != x) return 0;
@@ -81,203 +83,289 @@ __device__ __forceinline__ void f4_log_row(float* dst, const xf* row, int lo, in
     dst[x] = (row && x >= lo && x <= hi) ? xf_log(row[x - lo]) : -__builtin_inff();
 }
 
-// one cell: sum over classes of src[x -/+ d_i] (x) w[i], class order (oracle f4_cell_sum).
-// FWD: alpha (source total x - d_i, product a.m * w.m); else beta (x + d_i, w.m * b.m).
-template <bool FWD>
-__device__ __forceinline__ xf f4_cell(int x, const int* dur, const xf* w, int D, const xf* src,
-                                      int slo, int shi) {
+// one cell: sum over classes of src[x -/+ d_i] (x) w[i] (oracle f4_cell_sum). FWD: alpha
+// (source total x - d_i, product a.m * w.m); else beta (x + d_i, w.m * b.m). Classes padded to
+// DC = next power of two >= D with w = 0 and duration 0 (exact zero terms, as the oracle's
+// padding), so the 2 DC LDS reads of a cell issue back to back and the sum is the oracle's
+// pairwise tree (depth log2 DC instead of a DC-long add chain).
+template <bool FWD, int DC>
+__device__ __forceinline__ xf f4_cell(int x, const int* dur, const xf* w, const xf* src, int slo,
+                                      int shi) {
+  float m[DC];
+  int e[DC];
   int em = XF_EZERO;
-  for (int i = 0; i < D; ++i) {
-    const int y = FWD ? x - dur[i] : x + dur[i];
-    const bool in = y >= slo && y <= shi;
-    const int e = in ? src[in ? y - slo : 0].e + w[i].e : XF_EZERO;
-    em = max(em, e);
+  const unsigned span = (unsigned)(shi - slo);  // (an empty window: every term out)
+#pragma unroll
+  for (int i = 0; i < DC; ++i) {
+    const unsigned yr = (unsigned)((FWD ? x - dur[i] : x + dur[i]) - slo);
+    const bool in = shi >= slo && yr <= span;
+    const xf v = src[in ? yr : 0];
+    const xf ww = w[i];
+    m[i] = in ? (FWD ? v.m * ww.m : ww.m * v.m) : 0.0f;
+    e[i] = in ? v.e + ww.e : XF_EZERO;
+    em = max(em, e[i]);
   }
-  float s = 0.0f;
-  for (int i = 0; i < D; ++i) {
-    const int y = FWD ? x - dur[i] : x + dur[i];
-    const bool in = y >= slo && y <= shi;
-    const xf v = src[in ? y - slo : 0];
-    const float m = in ? (FWD ? v.m * w[i].m : w[i].m * v.m) : 0.0f;
-    const int e = in ? v.e + w[i].e : XF_EZERO;
-    s = s + xldexp(m, e - em);
+#pragma unroll
+  for (int i = 0; i < DC; ++i) m[i] = xldexp(m[i], e[i] - em);
+#pragma unroll
+  for (int len = DC; len > 1; len >>= 1) {
+#pragma unroll
+    for (int i = 0; i < len / 2; ++i) m[i] = m[2 * i] + m[2 * i + 1];
   }
-  return xf_norm(s, em);
+  return xf_norm(m[0], em);
 }
 
-// xor butterfly over the 64 lane partials (xf_add is commutative: every lane ends equal)
+// workgroup barrier ordering LDS only: __syncthreads() would also wait for every global store
+// in flight (vmcnt(0)), i.e. one HBM write round trip per sweep step; nothing in these kernels
+// reads back global memory written in the same launch
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int CTRL>
+__device__ __forceinline__ xf dpp_xf(xf v) {
+  return xf{__builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v.m), CTRL, 0xf, 0xf, false)),
+            __builtin_amdgcn_update_dpp(0, v.e, CTRL, 0xf, 0xf, false)};
+}
+__device__ __forceinline__ xf f4_add(xf a, xf b) { return xf_add(a.m, a.e, b.m, b.e); }
+
+// xor butterfly over the 64 lane partials, = the oracle's xor 1, 2, 4, ..., 32 (xf_add is
+// commutative, so every lane ends equal). Once a quad (8-group) is uniform, the half-mirror
+// (mirror) partner holds the xor-4 (xor-8) partner's value, so those two levels are DPP moves.
+// Whole wave active (no divergent caller).
 __device__ __forceinline__ xf f4_butterfly(xf acc) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float om = __shfl_xor(acc.m, off);
-    const int oe = __shfl_xor(acc.e, off);
-    acc = xf_add(acc.m, acc.e, om, oe);
-  }
+  acc = f4_add(acc, dpp_xf<0xB1>(acc));   // quad_perm [1,0,3,2]: xor 1
+  acc = f4_add(acc, dpp_xf<0x4E>(acc));   // quad_perm [2,3,0,1]: xor 2
+  acc = f4_add(acc, dpp_xf<0x141>(acc));  // row_half_mirror: xor 4
+  acc = f4_add(acc, dpp_xf<0x140>(acc));  // row_mirror: xor 8
+  acc = f4_add(acc, xf{__builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, acc.m), 0x401F)),
+                       __builtin_amdgcn_ds_swizzle(acc.e, 0x401F)});  // xor 16
+  acc = f4_add(acc, xf{__shfl_xor(acc.m, 32), __shfl_xor(acc.e, 32)});  // xor 32
   return acc;
 }
 
-__global__ __launch_bounds__(kF4Threads) void k_v2_fwd_bwd(V2FwdBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ xf z_sh;
-  __shared__ int bad_sh;
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int D = a.D, X = a.X, Imax = a.Imax, Wc = a.Wcap;
-  int* dur = reinterpret_cast<int*>(smem);
-  xf* wbuf = reinterpret_cast<xf*>(smem + ((D * 4 + 15) & ~15));  // [2][D]
-  xf* rowA = wbuf + 2 * D;                                          // [2][Wc]
-  xf* rowB = rowA + 2 * Wc;                                         // [2][Wc]
-  const float* lg = a.logits + (size_t)b * Imax * D;
-  float* g = a.grad ? a.grad + (size_t)b * Imax * D : nullptr;
-  const size_t drow = (size_t)(Imax + 1) * X;
-  float* la = a.log_alpha ? a.log_alpha + b * drow : nullptr;
-  float* lb = a.log_beta ? a.log_beta + b * drow : nullptr;
-  xf* ws = reinterpret_cast<xf*>(a.workspace) + (size_t)b * (Imax + 1) * Wc;
-  const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
-
-  if (tid == 0) bad_sh = 0;
-  for (int i = tid; i < D; i += kF4Threads) dur[i] = a.table[i];
-  __syncthreads();
-  F4Utt u;
+// per-utterance state both kernels derive the same way; false: no lattice (loss written by
+// the forward sweep, every output row zero / -inf)
+__device__ __forceinline__ bool f4_setup(const V2FwdBwdArgs& a, int b, const int* dur, F4Utt& u,
+                                         bool report) {
   u.I = a.input_length[b];
   u.O = a.output_length[b];
-  u.X = X;
+  u.X = a.X;
   u.test = a.test_mode;
   u.dmax = 0;
   bool neg = false;
-  for (int i = 0; i < D; ++i) {
+  for (int i = 0; i < a.D; ++i) {
     u.dmax = max(u.dmax, dur[i]);
     neg |= dur[i] < 0;
   }
-  const bool bad_len = u.I < 0 || u.I > Imax || u.O < 0;
-  if ((bad_len || neg) && tid == 0 && a.status) atomicOr(a.status, neg ? kStatusBadIndex : kStatusBadLength);
-  // every gradient row starts at zero (rows t < I are overwritten by the backward sweep)
-  if (g)
-    for (int k = tid; k < Imax * D; k += kF4Threads) g[k] = 0.0f;
-  auto finish_debug = [&](int r0, bool alpha_too) {  // rows r0..Imax of the debug outputs: -inf
-    for (int r = r0; r <= Imax; ++r) {
-      if (alpha_too && la) f4_log_row(la + (size_t)r * X, nullptr, 0, -1, X);
-      if (lb) f4_log_row(lb + (size_t)r * X, nullptr, 0, -1, X);
+  const bool bad_len = u.I < 0 || u.I > a.Imax || u.O < 0;
+  if (report && (bad_len || neg) && threadIdx.x == 0 && a.status)
+    atomicOr(a.status, neg ? kStatusBadIndex : kStatusBadLength);
+  return !(bad_len || neg || u.I == 0);
+}
+
+// workspace: alpha rows [B][Imax+1][Wc] | beta rows [B][Imax+1][Wc] | Z [B]
+struct F4Ws {
+  xf *alpha, *beta, *z;
+};
+__device__ __forceinline__ F4Ws f4_ws(const V2FwdBwdArgs& a) {
+  xf* base = reinterpret_cast<xf*>(a.workspace);
+  const size_t rows = (size_t)a.B * (a.Imax + 1) * a.Wcap;
+  return F4Ws{base, base + rows, base + 2 * rows};
+}
+
+template <int DC>
+__global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const bool fwd = blockIdx.y == 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int D = a.D, X = a.X, Imax = a.Imax, Wc = a.Wcap;
+  constexpr int Dp = DC;  // class slots padded to DC (zero weight, duration 0)
+  int* dur = reinterpret_cast<int*>(smem);
+  xf* wbuf = reinterpret_cast<xf*>(smem + ((Dp * 4 + 15) & ~15));  // [2][Dp]
+  xf* row = wbuf + 2 * Dp;                                            // [2][Wc]
+  const float* lg = a.logits + (size_t)b * Imax * D;
+  const size_t drow = (size_t)(Imax + 1) * X;
+  float* la = a.log_alpha ? a.log_alpha + b * drow : nullptr;
+  const F4Ws W = f4_ws(a);
+  xf* ws = (fwd ? W.alpha : W.beta) + (size_t)b * (Imax + 1) * Wc;
+  const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
+
+  for (int i = tid; i < Dp; i += kF4Threads) {
+    dur[i] = i < D ? a.table[i] : 0;
+    if (i >= D) wbuf[i] = wbuf[Dp + i] = xf_zero();
+  }
+  lds_sync();
+  F4Utt u;
+  if (!f4_setup(a, b, dur, u, fwd)) {
+    if (fwd) {
+      if (tid == 0) a.loss[b] = inf_loss;
+      if (la)
+        for (int r = 0; r <= Imax; ++r) f4_log_row(la + (size_t)r * X, nullptr, 0, -1, X);
     }
-  };
-  if (bad_len || neg || u.I == 0) {
-    if (tid == 0) a.loss[b] = inf_loss;
-    finish_debug(0, true);
     return;
   }
   const int I = u.I;
+  int dr[DC];  // durations in registers (VGPRs: the SGPR file is full with addresses)
+#pragma unroll
+  for (int i = 0; i < DC; ++i) dr[i] = dur[i];
   auto cls_ok = [&](int i) { return a.allow_skip || i != a.zid; };
-
-  // ================================ forward sweep ==========================================
-  int plo = 0, phi = 0;
-  if (tid == 0) {
-    rowA[0] = xf{0.5f, 1};
-    ws[0] = xf{0.5f, 1};
+  // class log-probs are staged through LDS in chunks of CH sweep steps (one global round trip
+  // per chunk, none inside a step: a load consumed inside the step loop would make every step
+  // wait for the ring stores before it, vmcnt counting both)
+  constexpr int CH = 64;  // = a.chunk
+  float* chunk = reinterpret_cast<float*>(row + 2 * Wc);  // [2][CH][D]
+  auto st = [&](int k) { return fwd ? k : I - 1 - k; };  // input step of sweep step k
+  auto stage = [&](int c) {  // chunk c = sweep steps [c*CH, (c+1)*CH)
+    float* dstc = chunk + (c & 1) * CH * D;
+    for (int idx = tid; idx < CH * D; idx += kF4Threads) {
+      const int k = c * CH + idx / D;
+      dstc[idx] = k < I ? lg[(size_t)st(k) * D + idx % D] : 0.0f;
+    }
+  };
+  auto weights = [&](int k) {  // class weights of sweep step k into wbuf[k & 1]
+    const float* srcc = chunk + ((k >> 6) & 1) * CH * D + (k & 63) * D;
+    for (int i = tid; i < D; i += kF4Threads) wbuf[(k & 1) * Dp + i] = xf_exp(srcc[i], cls_ok(i));
+  };
+  stage(0);
+  stage(1);
+  lds_sync();
+  weights(0);
+  // first row: alpha[0] = 1 at total 0; beta[I] = 1 over window(I)
+  int plo, phi;
+  f4_window(u, fwd ? 0 : I, plo, phi);
+  if (phi - plo + 1 > Wc) {
+    if (tid == 0 && a.status) atomicOr(a.status, kStatusBadLength);
+    return;
   }
-  for (int i = tid; i < D; i += kF4Threads) wbuf[i] = xf_exp(lg[i], cls_ok(i));
-  __syncthreads();
-  if (la) f4_log_row(la, rowA, 0, 0, X);
-  for (int r = 1; r <= I; ++r) {
+  for (int k = tid; k <= phi - plo; k += kF4Threads) {
+    row[k] = xf{0.5f, 1};
+    ws[(size_t)(fwd ? 0 : I) * Wc + k] = xf{0.5f, 1};
+  }
+  lds_sync();
+  if (fwd && la) f4_log_row(la, row, 0, 0, X);
+  for (int k = 1; k <= I; ++k) {
+    const int r = fwd ? k : I - k;  // row produced by this step
     int lo, hi;
     f4_window(u, r, lo, hi);
-    if (hi - lo + 1 > Wc) {  // host sizing bug: report, drop the utterance (uniform branch)
+    if (hi - lo + 1 > Wc) {  // host sizing bug: report, poison the loss (uniform branch)
       if (tid == 0) {
         if (a.status) atomicOr(a.status, kStatusBadLength);
-        a.loss[b] = __builtin_nanf("");
+        if (fwd) a.loss[b] = __builtin_nanf("");
       }
-      finish_debug(r, true);
       return;
     }
-    const xf* w = wbuf + ((r - 1) & 1) * D;
-    if (r < I)
-      for (int i = tid; i < D; i += kF4Threads) wbuf[(r & 1) * D + i] = xf_exp(lg[(size_t)r * D + i], cls_ok(i));
-    const xf* src = rowA + ((r - 1) & 1) * Wc;
-    xf* dst = rowA + (r & 1) * Wc;
+    if ((k & 63) == 0) stage((k >> 6) + 1);  // first read CH = 64 steps (barriers) from now
+    if (k < I) weights(k);                     // for the next iteration
+    const xf* w = wbuf + ((k - 1) & 1) * Dp;
+    const xf* src = row + ((k - 1) & 1) * Wc;
+    xf* dst = row + (k & 1) * Wc;
     xf* wrow = ws + (size_t)r * Wc;
     for (int x = lo + tid; x <= hi; x += kF4Threads) {
-      const xf v = f4_cell<true>(x, dur, w, D, src, plo, phi);
+      const xf v = fwd ? f4_cell<true, DC>(x, dr, w, src, plo, phi)
+                       : f4_cell<false, DC>(x, dr, w, src, plo, phi);
       dst[x - lo] = v;
       wrow[x - lo] = v;
     }
-    __syncthreads();
-    if (la) f4_log_row(la + (size_t)r * X, dst, lo, hi, X);
+    lds_sync();
+    if (fwd && la) f4_log_row(la + (size_t)r * X, dst, lo, hi, X);
     plo = lo;
     phi = hi;
   }
+  if (!fwd) return;
   if (la)
     for (int r = I + 1; r <= Imax; ++r) f4_log_row(la + (size_t)r * X, nullptr, 0, -1, X);
-
-  // ================================ Z =======================================================
-  const int zlo = plo, zhi = phi;  // window(I)
+  // Z over window(I): lane partials x mod 64, butterfly
   if (wave == 0) {
     xf acc = xf_zero();
-    const xf* rI = rowA + (I & 1) * Wc;
-    for (int x = zlo + ((lane - zlo) & 63); x <= zhi; x += 64) {
-      const xf v = rI[x - zlo];
-      acc = xf_add(acc.m, acc.e, v.m, v.e);
-    }
+    const xf* rI = row + (I & 1) * Wc;
+    for (int x = plo + ((lane - plo) & 63); x <= phi; x += 64) acc = f4_add(acc, rI[x - plo]);
     acc = f4_butterfly(acc);
     if (lane == 0) {
-      z_sh = acc;
+      W.z[b] = acc;
       a.loss[b] = acc.m == 0.0f ? inf_loss : 0.0f - xf_log(acc);
     }
   }
-  __syncthreads();
-  const xf Z = z_sh;
-  if (Z.m == 0.0f) {
-    finish_debug(0, false);
+}
+
+constexpr int kF4GradThreads = 256;
+constexpr int kF4GradWaves = kF4GradThreads / 64;
+
+// gradients of step t = blockIdx.y (and the debug beta row t); rows t >= I: zeros / -inf
+template <int DC>
+__global__ __launch_bounds__(kF4GradThreads) void k_f4_grad(V2FwdBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x, t = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int D = a.D, X = a.X, Imax = a.Imax, Wc = a.Wcap;
+  int* dur = reinterpret_cast<int*>(smem);
+  xf* at = reinterpret_cast<xf*>(smem + ((D * 4 + 15) & ~15));  // alpha row t
+  xf* bn = at + Wc;                                                 // beta row t+1
+  float* g = a.grad ? a.grad + ((size_t)b * Imax + (t < Imax ? t : 0)) * D : nullptr;
+  float* lb = a.log_beta ? a.log_beta + ((size_t)b * (Imax + 1) + t) * X : nullptr;
+  const F4Ws W = f4_ws(a);
+  for (int i = tid; i < D; i += kF4GradThreads) dur[i] = a.table[i];
+  lds_sync();
+  F4Utt u;
+  const bool ok = f4_setup(a, b, dur, u, false);
+  const xf Z = ok ? W.z[b] : xf_zero();
+  const bool live = ok && Z.m != 0.0f;
+  if (lb) {
+    int lo = 0, hi = -1;
+    if (live && t <= u.I) f4_window(u, t, lo, hi);
+    const xf* br = W.beta + ((size_t)b * (Imax + 1) + t) * Wc;
+    for (int x = tid; x < X; x += kF4GradThreads)
+      lb[x] = (x >= lo && x <= hi) ? xf_log(br[x - lo]) : -__builtin_inff();
+  }
+  if (t >= Imax || !g) return;
+  if (!live || t >= u.I) {
+    for (int i = tid; i < D; i += kF4GradThreads) g[i] = 0.0f;
     return;
   }
+  int lo, hi, nlo, nhi;
+  f4_window(u, t, lo, hi);
+  f4_window(u, t + 1, nlo, nhi);
+  const xf* ga = W.alpha + ((size_t)b * (Imax + 1) + t) * Wc;
+  const xf* gb = W.beta + ((size_t)b * (Imax + 1) + t + 1) * Wc;
+  for (int k = tid; k <= hi - lo; k += kF4GradThreads) at[k] = ga[k];
+  for (int k = tid; k <= nhi - nlo; k += kF4GradThreads) bn[k] = gb[k];
+  lds_sync();
   const float izm = 1.0f / Z.m;
   const int ize = -Z.e;
-
-  // ================================ backward sweep =========================================
-  for (int x = zlo + tid; x <= zhi; x += kF4Threads) rowB[(I & 1) * Wc + x - zlo] = xf{0.5f, 1};
-  __syncthreads();
-  if (lb) {
-    f4_log_row(lb + (size_t)I * X, rowB + (I & 1) * Wc, zlo, zhi, X);
-    for (int r = I + 1; r <= Imax; ++r) f4_log_row(lb + (size_t)r * X, nullptr, 0, -1, X);
-  }
-  int nlo = zlo, nhi = zhi;  // window(t+1)
-  int lo, hi;
-  f4_window(u, I - 1, lo, hi);  // window(t)
-  for (int t = I - 1; t >= 0; --t) {
-    int plo2 = 0, phi2 = -1;  // window(t-1)
-    if (t >= 1) f4_window(u, t - 1, plo2, phi2);
-    // alpha row t-1 from HBM into the buffer that held row t+1; weights of step t-1
-    if (t >= 1) {
-      xf* pre = rowA + ((t - 1) & 1) * Wc;
-      const xf* srow = ws + (size_t)(t - 1) * Wc;
-      for (int k = tid; k <= phi2 - plo2; k += kF4Threads) pre[k] = srow[k];
-      for (int i = tid; i < D; i += kF4Threads) wbuf[((t - 1) & 1) * D + i] = xf_exp(lg[(size_t)(t - 1) * D + i], cls_ok(i));
+  auto emit = [&](int i, xf acc) {
+    const xf S = f4_butterfly(acc);
+    if (lane == 0) {
+      const xf w = xf_exp(a.logits[((size_t)b * Imax + t) * D + i], a.allow_skip || i != a.zid);
+      g[i] = xf_neg_post((S.m * w.m) * izm, S.e + w.e + ize);
     }
-    const xf* w = wbuf + (t & 1) * D;
-    const xf* bn = rowB + ((t + 1) & 1) * Wc;  // beta row t+1
-    const xf* at = rowA + (t & 1) * Wc;         // alpha row t
-    xf* bt = rowB + (t & 1) * Wc;
-    for (int y = lo + tid; y <= hi; y += kF4Threads) bt[y - lo] = f4_cell<false>(y, dur, w, D, bn, nlo, nhi);
-    // gradients of step t: class i on wave i % 4, destination totals x in lane partials
-    if (g) {
-      for (int i = wave; i < D; i += kF4Waves) {
-        xf acc = xf_zero();
-        const int di = dur[i];
-        for (int x = nlo + ((lane - nlo) & 63); x <= nhi; x += 64) {
-          const int y = x - di;
-          if (y < lo || y > hi) continue;
-          const xf av = at[y - lo], bv = bn[x - nlo];
-          acc = xf_add(acc.m, acc.e, av.m * bv.m, av.e + bv.e);
-        }
-        acc = f4_butterfly(acc);
-        if (lane == 0) g[(size_t)t * D + i] = xf_neg_post((acc.m * w[i].m) * izm, acc.e + w[i].e + ize);
-      }
-    }
-    __syncthreads();
-    if (lb) f4_log_row(lb + (size_t)t * X, bt, lo, hi, X);
-    nlo = lo;
-    nhi = hi;
-    lo = plo2;
-    hi = phi2;
+  };
+  constexpr int NCW = (DC + kF4GradWaves - 1) / kF4GradWaves;  // classes per wave
+  xf acc[NCW];
+  int di[NCW];
+#pragma unroll
+  for (int j = 0; j < NCW; ++j) {
+    acc[j] = xf_zero();
+    const int i = wave + j * kF4GradWaves;
+    di[j] = i < D ? dur[i] : 0;
   }
+  for (int x = nlo + ((lane - nlo) & 63); x <= nhi; x += 64) {
+    const xf bv = bn[x - nlo];
+#pragma unroll
+    for (int j = 0; j < NCW; ++j) {
+      // a term outside the window is an exact zero: adding it leaves a normalized (or zero)
+      // partial unchanged, so the select is the oracle's skip
+      const int y = x - di[j];
+      const bool in = y >= lo && y <= hi;
+      const xf av = at[in ? y - lo : 0];
+      acc[j] = xf_add(acc[j].m, acc[j].e, in ? av.m * bv.m : 0.0f, in ? av.e + bv.e : XF_EZERO);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NCW; ++j)
+    if (wave + j * kF4GradWaves < D) emit(wave + j * kF4GradWaves, acc[j]);  // wave-uniform
 }
 
 }  // namespace
@@ -291,7 +379,22 @@ size_t v2_fwd_bwd_wcap(int max_total, bool test_mode) {
 
 size_t v2_fwd_bwd_workspace_bytes(int B, int Imax, int max_total, bool test_mode) {
   if (B <= 0 || Imax <= 0 || max_total < 0) return 0;
-  return (size_t)B * (Imax + 1) * v2_fwd_bwd_wcap(max_total, test_mode) * sizeof(xf);
+  return (2 * (size_t)B * (Imax + 1) * v2_fwd_bwd_wcap(max_total, test_mode) + B) * sizeof(xf);
+}
+
+template <int DC>
+int launch_f4(const V2FwdBwdArgs& a, size_t lds, size_t glds, hipStream_t st) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_f4_sweep<DC>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_f4_sweep<DC>, dim3(a.B, 2), dim3(kF4Threads), lds, st, a);
+  if (hipGetLastError() != hipSuccess) return SSNT_ERR_HIP;
+  if (!a.grad && !a.log_beta) return SSNT_OK;
+  if (glds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_f4_grad<DC>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds);
+  hipLaunchKernelGGL(k_f4_grad<DC>, dim3(a.B, a.Imax + 1), dim3(kF4GradThreads), glds, st, a);
+  return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
 int launch_v2_fwd_bwd(const V2FwdBwdArgs& in, hipStream_t st) {
@@ -300,16 +403,22 @@ int launch_v2_fwd_bwd(const V2FwdBwdArgs& in, hipStream_t st) {
       !a.output_length || !a.loss)
     return SSNT_ERR_INVALID_ARG;
   if (a.B == 0) return SSNT_OK;
+  if (a.D > 64) return SSNT_ERR_UNSUPPORTED;  // cell sums unrolled over <= 64 classes
+  if ((size_t)a.B * (a.Imax + 1) > 0x7fffffffu / 2) return SSNT_ERR_UNSUPPORTED;
   a.Wcap = (int)v2_fwd_bwd_wcap(a.X - 1, a.test_mode);
-  const size_t lds = (size_t)((a.D * 4 + 15) & ~15) + 2 * (size_t)a.D * sizeof(xf) + 4 * (size_t)a.Wcap * sizeof(xf);
-  if (lds > 160 * 1024 - 1024) return SSNT_ERR_UNSUPPORTED;
+  const int Dp = a.D <= 8 ? 8 : a.D <= 16 ? 16 : a.D <= 32 ? 32 : 64;  // = DC
+  const size_t head = (size_t)((Dp * 4 + 15) & ~15);
+  a.chunk = 64;  // sweep steps per staged chunk (a power of two)
+  const size_t lds = head + 2 * (size_t)Dp * sizeof(xf) + 2 * (size_t)a.Wcap * sizeof(xf) +
+                     2 * (size_t)a.chunk * a.D * sizeof(float);
+  const size_t glds = head + 2 * (size_t)a.Wcap * sizeof(xf);
+  if (lds > 160 * 1024 - 1024 || glds > 160 * 1024 - 1024) return SSNT_ERR_UNSUPPORTED;
   if (!a.workspace || a.workspace_bytes < v2_fwd_bwd_workspace_bytes(a.B, a.Imax, a.X - 1, a.test_mode))
     return SSNT_ERR_WORKSPACE;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_v2_fwd_bwd),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_v2_fwd_bwd, dim3(a.B), dim3(kF4Threads), lds, st, a);
-  return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
+  if (a.D <= 8) return launch_f4<8>(a, lds, glds, st);
+  if (a.D <= 16) return launch_f4<16>(a, lds, glds, st);
+  if (a.D <= 32) return launch_f4<32>(a, lds, glds, st);
+  return launch_f4<64>(a, lds, glds, st);
 }
 
 }  // namespace ssnt
