@@ -16,4 +16,7 @@ timeout -k 10 300 python3 tools/bench_configs.py > gpurun_out/configs_${TAG}.jso
 cat gpurun_out/configs_${TAG}.jsonl
 timeout -k 10 200 python3 tools/bench_step_symbols.py > gpurun_out/steps_${TAG}.json 2> gpurun_out/steps_${TAG}.err
 cat gpurun_out/steps_${TAG}.json
+timeout -k 10 200 python3 tools/bench_cliff.py > gpurun_out/cliff_${TAG}.jsonl 2> gpurun_out/cliff_${TAG}.err
+cat gpurun_out/cliff_${TAG}.jsonl
 bash tools/profile_gpu.sh "$TAG"
+bash tools/profile_long.sh "$TAG"
