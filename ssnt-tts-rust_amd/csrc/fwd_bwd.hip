@@ -339,7 +339,10 @@ int variant() {
 size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
   // the segmented kernel keeps its rows (plus beta at the cut) in the workspace at every T; one
   // size serves every kernel variant (the two-wave kernel needs B*T*U xf at most)
-  return fwd_bwd_wide_workspace_bytes(B, T, U);
+  // (the streaming kernel's narrow form pads rows to whole lane slices: U + 3 at most)
+  const size_t wide = fwd_bwd_wide_workspace_bytes(B, T, U);
+  const size_t stream = (size_t)B * T * ((size_t)U + 3) * sizeof(xf);
+  return wide > stream ? wide : stream;
 }
 
 int set_fwd_bwd_variant(int v) {
@@ -375,9 +378,8 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;
     summed = false;
-    // long rows, and the shapes the streaming kernel declines (U % K != 0, offset or unaligned
-    // tensors): the segmented kernel takes any U <= 1024 at 8-byte alignment (loss sum: the
-    // separate pass)
+    // long rows, and what the streaming kernel declines (4-byte-aligned log_trans / grad): the
+    // segmented kernel takes any U <= 1024 at 8-byte alignment (loss sum: the separate pass)
     if (a.workspace && a.workspace_bytes >= fwd_bwd_wide_workspace_bytes(a.B, a.T, a.U)) {
       rc = launch_fwd_bwd_wide(a, st, true);
       if (rc != SSNT_ERR_UNSUPPORTED) return rc;

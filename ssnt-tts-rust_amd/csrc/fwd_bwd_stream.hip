@@ -328,7 +328,30 @@ __device__ __forceinline__ void lds_xrow_st(xf* p, const XRow<K>& r) {
   st_vec<2 * K>(reinterpret_cast<float*>(p), v);
 }
 
-template <int K, bool OBS, bool LDS, int kNC, int kNH, int kRingSel>
+// Global accesses of a lane's K positions, F floats per position. NV (narrow): one access per
+// position -- U % K != 0 or 8-byte-aligned tensors: a slice may straddle the row end, and each
+// position is then entirely inside the row's buffer range or entirely outside it (reads 0,
+// stores dropped). Otherwise one vector access per slice.
+template <int K, int F, bool NV>
+__device__ __forceinline__ void gld(float* dst, __amdgpu_buffer_rsrc_t r, int p0) {
+  if constexpr (NV) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) buf_ld<F>(dst + F * j, r, (p0 + j) * 4 * F);
+  } else {
+    buf_ld<F * K>(dst, r, p0 * 4 * F);
+  }
+}
+template <int K, int F, bool NV>
+__device__ __forceinline__ void gst(const float* v, __amdgpu_buffer_rsrc_t r, int p0) {
+  if constexpr (NV) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) buf_st<F>(v + F * j, r, (p0 + j) * 4 * F);
+  } else {
+    buf_st<F * K>(v, r, p0 * 4 * F);
+  }
+}
+
+template <int K, bool OBS, bool LDS, int kNC, int kNH, int kRingSel, bool NV>
 __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream(FwdBwdArgs a) {
   constexpr int kWaves = 2 + 2 * kNC + 2 * kNH;
   // kRingSel: ring slots (0 = default); tuning variants: +100 publish every step past the cut,
@@ -342,6 +365,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   const Role role = role_of<kNC, kNH>(wave);
   const int lane = threadIdx.x & 63;
   const int T = a.T, U = a.U;
+  const int Up = NV ? K * ((U + K - 1) / K) : U;  // internal row stride: whole lane slices
   const int S = a.step_len[b];
   const int P = a.pos_len[b];
   const bool term = (a.flags & SSNT_FLAG_TERMINAL_EMIT) != 0;
@@ -354,18 +378,18 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   float* lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
   const int p0 = K * lane;
   const bool act = p0 < U;
-  const int pr = act ? p0 : U - K;  // LDS read position (clamped for lanes past U)
+  const int pr = act ? p0 : Up - K;  // LDS read position (clamped for lanes past U)
 
   // ---- LDS: ctl | cut (64K xf) | junk (64 x 16K B) | input rings [2][R] | chain-row rings
   //      [2][kR2][U xf] | storage rows [T][U xf] (LDS mode)
   Ctl* ctl = reinterpret_cast<Ctl*>(smem);
   xf* cutb = reinterpret_cast<xf*>(smem + kCtlBytes);
   unsigned char* junk = reinterpret_cast<unsigned char*>(cutb + 64 * K);
-  const int slot_bytes = (U * 16 + (OBS ? U * 8 : 0) + 15) & ~15;
-  const int nl16 = (U / K) * 16;  // bytes of one element block of a slot (U % K == 0)
+  const int slot_bytes = (Up * 16 + (OBS ? Up * 8 : 0) + 15) & ~15;
+  const int nl16 = (Up / K) * 16;  // bytes of one element block of a slot
   unsigned char* inr = junk + 64 * 16 * K;
   xf* outr = reinterpret_cast<xf*>(inr + 2 * R * slot_bytes);
-  xf* rows = LDS ? outr + 2 * kR2 * U : reinterpret_cast<xf*>(a.workspace) + (size_t)b * TU;
+  xf* rows = LDS ? outr + 2 * kR2 * Up : reinterpret_cast<xf*>(a.workspace) + (size_t)b * T * Up;
   unsigned char* junk_lane = junk + 16 * K * lane;
 
   auto fill_rows = [&](int from, int w0, int wstep) {  // zero grads / -inf debug rows
@@ -375,10 +399,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 #pragma unroll
     for (int j = 0; j < K; ++j) ninf[j] = -__builtin_inff();
     for (int s = from + w0; s < T; s += wstep) {
-      if (g) buf_st<2 * K>(z, brsrc(g + (size_t)s * U * 2, U * 8u), p0 * 8);
-      if (go) buf_st<K>(z, brsrc(go + (size_t)s * U, U * 4u), p0 * 4);
-      if (la) buf_st<K>(ninf, brsrc(la + (size_t)s * U, U * 4u), p0 * 4);
-      if (lb) buf_st<K>(ninf, brsrc(lb + (size_t)s * U, U * 4u), p0 * 4);
+      if (g) gst<K, 2, NV>(z, brsrc(g + (size_t)s * U * 2, U * 8u), p0);
+      if (go) gst<K, 1, NV>(z, brsrc(go + (size_t)s * U, U * 4u), p0);
+      if (la) gst<K, 1, NV>(ninf, brsrc(la + (size_t)s * U, U * 4u), p0);
+      if (lb) gst<K, 1, NV>(ninf, brsrc(lb + (size_t)s * U, U * 4u), p0);
     }
   };
   const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
@@ -399,19 +423,19 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // storage rows: LDS, or this utterance's workspace rows through range-checked buffer ops
   auto row_st = [&](int s, const XRow<K>& r) {
     if constexpr (LDS) {
-      lds_xrow_st<K>(act ? rows + (size_t)s * U + p0 : reinterpret_cast<xf*>(junk_lane), r);
+      lds_xrow_st<K>(act ? rows + (size_t)s * Up + p0 : reinterpret_cast<xf*>(junk_lane), r);
     } else {
       float v[2 * K];
       xrow_pack<K>(r, v);
-      buf_st<2 * K>(v, brsrc(rows + (size_t)s * U, U * 8u), p0 * 8);
+      buf_st<2 * K>(v, brsrc(rows + (size_t)s * Up, Up * 8u), p0 * 8);
     }
   };
   auto row_ld = [&](int s) {
     if constexpr (LDS) {
-      return lds_xrow<K>(rows + (size_t)s * U + pr);
+      return lds_xrow<K>(rows + (size_t)s * Up + pr);
     } else {
       float v[2 * K];
-      buf_ld<2 * K>(v, brsrc(rows + (size_t)s * U, U * 8u), pr * 8);
+      buf_ld<2 * K>(v, brsrc(rows + (size_t)s * Up, Up * 8u), pr * 8);
       return xrow_unpack<K>(v);
     }
   };
@@ -531,15 +555,15 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         in.Sh.m[q] = v[4 * q + 2];
         in.Sh.e[q] = __builtin_bit_cast(int, v[4 * q + 3]);
       }
-      if constexpr (OBS) in.O = lds_xrow<K>(reinterpret_cast<const xf*>(sl + 16 * U) + pr);
+      if constexpr (OBS) in.O = lds_xrow<K>(reinterpret_cast<const xf*>(sl + 16 * Up) + pr);
       if (d == 0) {
-        in.A = (s == M) ? row_ld(M) : lds_xrow<K>(outr + (size_t)(s % kR2) * U + pr);
+        in.A = (s == M) ? row_ld(M) : lds_xrow<K>(outr + (size_t)(s % kR2) * Up + pr);
         in.Bn = row_ld(min(s + 1, S - 1));  // (terminal transition: unused)
         if (OBS || lb) in.Bs = (s == M) ? lds_xrow<K>(cutb + pr) : row_ld(s);
       } else {
         in.A = row_ld(s);  // beta[s] is ring row r % kR2 (r = S-1-s), beta[s+1] ring row (r-1)
-        in.Bn = (s + 1 == M) ? lds_xrow<K>(cutb + pr) : lds_xrow<K>(outr + (size_t)(kR2 + (r - 1) % kR2) * U + pr);
-        if (OBS || lb) in.Bs = lds_xrow<K>(outr + (size_t)(kR2 + r % kR2) * U + pr);
+        in.Bn = (s + 1 == M) ? lds_xrow<K>(cutb + pr) : lds_xrow<K>(outr + (size_t)(kR2 + (r - 1) % kR2) * Up + pr);
+        if (OBS || lb) in.Bs = lds_xrow<K>(outr + (size_t)(kR2 + r % kR2) * Up + pr);
       }
       cbar();
       ctr_st(&ctl->help[d][h], i + 1);  // ring rows read (in-order DS): reusable
@@ -602,9 +626,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
               if constexpr (OBS) gob[q] = xf_neg_post((A.m[q] * Bs.m[q]) * izm, ae + Bs.e[q]);
             }
           }
-          if (g && !EXP(1)) buf_st<2 * K>(ge, brsrc(g + (size_t)s * U * 2, U * 8u), p0 * 8);
+          if (g && !EXP(1)) gst<K, 2, NV>(ge, brsrc(g + (size_t)s * U * 2, U * 8u), p0);
           if constexpr (OBS) {
-            if (go) buf_st<K>(gob, brsrc(go + (size_t)s * U, U * 4u), p0 * 4);
+            if (go) gst<K, 1, NV>(gob, brsrc(go + (size_t)s * U, U * 4u), p0);
           }
           if (la || lb) {  // debug outputs (slow path)
             float va[K], vb[K];
@@ -613,8 +637,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
               va[q] = zero_z ? -__builtin_inff() : xf_log(xf_norm(A.m[q], A.e[q]));  // (lazy rows)
               vb[q] = zero_z ? -__builtin_inff() : xf_log(xf_norm(Bs.m[q], Bs.e[q]));
             }
-            if (la) buf_st<K>(va, brsrc(la + (size_t)s * U, U * 4u), p0 * 4);
-            if (lb) buf_st<K>(vb, brsrc(lb + (size_t)s * U, U * 4u), p0 * 4);
+            if (la) gst<K, 1, NV>(va, brsrc(la + (size_t)s * U, U * 4u), p0);
+            if (lb) gst<K, 1, NV>(vb, brsrc(lb + (size_t)s * U, U * 4u), p0);
           }
     };
     auto row = [&](int i, GIn& cur, GIn& nxt) {
@@ -656,10 +680,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         return;
       }
       const int row = min(max(d == 0 ? r : S - 1 - r, 0), T - 1);
-      buf_ld<2 * K>(it.lt, brsrc(lt + (size_t)row * U * 2, U * 8u), p0 * 8);
+      gld<K, 2, NV>(it.lt, brsrc(lt + (size_t)row * U * 2, U * 8u), p0);
       if constexpr (OBS) {
         const int orow = min(row + 1, T - 1);
-        buf_ld<K>(it.ob, brsrc(lo + (size_t)orow * U, U * 4u), p0 * 4);
+        gld<K, 1, NV>(it.ob, brsrc(lo + (size_t)orow * U, U * 4u), p0);
       }
     };
     Item<K, OBS> pf[D];
@@ -728,7 +752,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           if constexpr (OBS) {
             float o[2 * K];
             xrow_pack<K>(O, o);
-            st_vec<2 * K>(reinterpret_cast<float*>(act ? sl + 16 * U + 8 * p0 : junk_lane), o);
+            st_vec<2 * K>(reinterpret_cast<float*>(act ? sl + 16 * Up + 8 * p0 : junk_lane), o);
           }
           cbar();
           ctr_st(&ctl->conv[d][c], k + 1);
@@ -770,7 +794,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   xf* optr[kR2];  // chain-row ring row j, this lane (junk past U)
 #pragma unroll
   for (int j = 0; j < kR2; ++j)
-    optr[j] = act ? outr + (size_t)(d * kR2 + j) * U + p0 : reinterpret_cast<xf*>(junk_lane);
+    optr[j] = act ? outr + (size_t)(d * kR2 + j) * Up + p0 : reinterpret_cast<xf*>(junk_lane);
   auto rd = [&](int j, XRow<K>& E, XRow<K>& Xx, XRow<K>& O) {
     float v[4 * K];
 #pragma unroll
@@ -783,7 +807,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       Xx.e[q] = __builtin_bit_cast(int, v[4 * q + 3]);
     }
     if constexpr (OBS) {
-      O = lds_xrow<K>(reinterpret_cast<const xf*>(sptr[j] - 16 * (pr / K) + 16 * U) + pr);
+      O = lds_xrow<K>(reinterpret_cast<const xf*>(sptr[j] - 16 * (pr / K) + 16 * Up) + pr);
     } else {
 #pragma unroll
       for (int q = 0; q < K; ++q) {
@@ -837,8 +861,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     sfor<PF>([&](auto J) { rd(decltype(J)::value, Eb[decltype(J)::value], Xb[decltype(J)::value], Ob[decltype(J)::value]); });
     int help_seen = M + 1;  // first alpha ring row not yet released by the gradient waves
     // storage write pointer for alpha[r+1] (LDS mode)
-    xf* wp = act ? rows + (size_t)U + p0 : reinterpret_cast<xf*>(junk_lane);
-    const int wstep = act ? U : 0;
+    xf* wp = act ? rows + (size_t)Up + p0 : reinterpret_cast<xf*>(junk_lane);
+    const int wstep = act ? Up : 0;
     // steps [r0, r1): rows up to r1+1 converted; phase 2: ring rows up to r1-kR2 released
     auto hwait = [&](int r0, int r1, bool phase2) {
       (void)r0;
@@ -889,8 +913,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     cbar();
     sfor<PF>([&](auto J) { rd(decltype(J)::value, Eb[decltype(J)::value], Xb[decltype(J)::value], Ob[decltype(J)::value]); });
     int help_seen = S - M;  // first beta gradient row (stream rows) not finished
-    xf* wp = act ? rows + (size_t)(S - 1) * U + p0 : reinterpret_cast<xf*>(junk_lane);  // beta[S-1-r]
-    const int wstep = act ? U : 0;
+    xf* wp = act ? rows + (size_t)(S - 1) * Up + p0 : reinterpret_cast<xf*>(junk_lane);  // beta[S-1-r]
+    const int wstep = act ? Up : 0;
     // stream row r -> kind 0: storage row S-1-r; 1: cut buffer; 2: ring row r % kR2
     auto put = [&](int r, int i, auto Kd) {
       constexpr int kind = decltype(Kd)::value;
@@ -956,10 +980,11 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+inline bool aligned_to(const void* p, uintptr_t m) { return (reinterpret_cast<uintptr_t>(p) & (m - 1)) == 0; }
 
-template <int K, bool OBS, bool LDS, int NC, int NH, int RS>
+template <int K, bool OBS, bool LDS, int NC, int NH, int RS, bool NV>
 int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
-  auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH, RS>;
+  auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH, RS, NV>;
   // dynamic LDS above 64 KiB needs the attribute; it is per device, so it is set on every such
   // launch (a host-side call, no device work) rather than cached in a process-wide flag
   if (lds > 64 * 1024)
@@ -971,19 +996,27 @@ int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
 
 template <int K, bool OBS, int NC, int NH, int RS = 0>
 int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
-  // whole lane slices and 16-byte aligned tensors (the kernel's vector accesses)
+  // whole lane slices and 16-byte aligned tensors: the vector form; else (U % K != 0, or
+  // tensors at 8-byte (trans, grad) / 4-byte (the rest) alignment) the narrow form
   const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
                    aligned16(a.grad) && aligned16(a.grad_obs) && aligned16(a.log_alpha) &&
                    aligned16(a.log_beta) && aligned16(a.workspace);
-  if (!vec) return SSNT_ERR_UNSUPPORTED;
+  const bool narrow_ok = aligned_to(a.log_trans, 8) && aligned_to(a.grad, 8) && aligned16(a.workspace) &&
+                         aligned_to(a.log_obs, 4) && aligned_to(a.grad_obs, 4) &&
+                         aligned_to(a.log_alpha, 4) && aligned_to(a.log_beta, 4);
+  if (!vec && !narrow_ok) return SSNT_ERR_UNSUPPORTED;
+  const int Up = K * ((a.U + K - 1) / K);
   const size_t head = stream_head_bytes(K, a.U, OBS, RS);
   if (head > kLdsBudget) return SSNT_ERR_UNSUPPORTED;
-  const size_t rows = (size_t)a.T * a.U * sizeof(xf);
+  const size_t rows = (size_t)a.T * (vec ? a.U : Up) * sizeof(xf);
   const bool lds = head + rows <= kLdsBudget;
   if (!lds && (a.workspace == nullptr || a.workspace_bytes < (size_t)a.B * rows))
     return SSNT_ERR_WORKSPACE;
-  return lds ? launch_stream_kernel<K, OBS, true, NC, NH, RS>(a, head + rows, st)
-             : launch_stream_kernel<K, OBS, false, NC, NH, RS>(a, head, st);
+  if (vec)
+    return lds ? launch_stream_kernel<K, OBS, true, NC, NH, RS, false>(a, head + rows, st)
+               : launch_stream_kernel<K, OBS, false, NC, NH, RS, false>(a, head, st);
+  return lds ? launch_stream_kernel<K, OBS, true, NC, NH, RS, true>(a, head + rows, st)
+             : launch_stream_kernel<K, OBS, false, NC, NH, RS, true>(a, head, st);
 }
 
 template <bool OBS>
@@ -1022,9 +1055,10 @@ size_t stream_head_bytes(int K, int U, bool obs, int ring) {
   const int R = ring ? ring : obs ? in_slots<true>() : in_slots<false>();
   const int R2o = obs ? out_slots<true>() : out_slots<false>();
   const int R2 = R2o < R ? R2o : R;
-  const size_t slot = ((size_t)U * 16 + (obs ? (size_t)U * 8 : 0) + 15) & ~(size_t)15;
+  const size_t Up = (size_t)K * ((U + K - 1) / K);  // (= U when U % K == 0)
+  const size_t slot = (Up * 16 + (obs ? Up * 8 : 0) + 15) & ~(size_t)15;
   return kCtlBytes + (size_t)64 * K * sizeof(xf) + (size_t)64 * 16 * K + 2 * (size_t)R * slot +
-         2 * (size_t)R2 * U * sizeof(xf);
+         2 * (size_t)R2 * Up * sizeof(xf);
 }
 
 #ifdef SSNT_EXP

@@ -306,11 +306,11 @@ def test_rows_beyond_512_bit_exact(gpu, oracle, kernel_variant, shape):
 
 
 @pytest.mark.parametrize("shift", [1, 2, 4])
-@pytest.mark.parametrize("U", [80, 81])
+@pytest.mark.parametrize("U", [80, 81, 127, 33])
 def test_offset_and_odd_shapes(gpu, oracle, kernel_variant, shift, U):
     # tensors at an element offset (4 / 8 / 16-byte aligned bases) and U % K != 0: the streaming
-    # kernel declines what it cannot vector-load and the segmented / two-wave kernels take over
-    # with identical bits
+    # kernel's narrow form takes U % K != 0 and 8-byte alignment, the two-wave kernel 4-byte
+    # alignment -- with identical bits
     dev = torch.device("cuda:0")
     B, T = 5, 90
     lt = oracle.synth_log_trans(B, T, U, seed=shift + U)

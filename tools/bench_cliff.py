@@ -41,7 +41,7 @@ def case(B, T, U, shift, variant):
 
 
 if __name__ == "__main__":
-    for (B, T, U, shift) in [(256, 200, 80, 0), (256, 200, 81, 0), (256, 200, 80, 1),
+    for (B, T, U, shift) in [(256, 200, 80, 0), (256, 200, 81, 0), (256, 200, 127, 0), (256, 200, 80, 1),
                              (256, 200, 80, 2), (256, 200, 120, 0), (64, 400, 700, 0),
                              (64, 400, 1024, 0)]:
         for v in (0, 1):
