@@ -312,7 +312,7 @@ def test_offset_and_odd_shapes(gpu, oracle, kernel_variant, shift, U):
     # kernel's narrow form takes U % K != 0 and 8-byte alignment, the two-wave kernel 4-byte
     # alignment -- with identical bits
     dev = torch.device("cuda:0")
-    B, T = 5, 90
+    B, T = 5, max(90, U + 10)
     lt = oracle.synth_log_trans(B, T, U, seed=shift + U)
     rng = np.random.default_rng(shift)
     P = [U] + [int(x) for x in rng.integers(1, U + 1, size=B - 1)]
