@@ -21,6 +21,8 @@
 // beam has u == s, so its row is lattice[b,s]); rows are prefetched kAhead steps ahead.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "decode_dev.h"
 
 namespace ssnt {
@@ -38,20 +40,26 @@ constexpr int kRing = 7;     // staged output arrays
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
 // LDS layout of k_fused_reg (bytes), shared with the host launcher.
+// WHOLE: the staged outputs of all T steps fit, so they are flushed once after the loop -- no
+// global store inside the step loop, whose wait-count merge would otherwise turn the row
+// prefetch's wait into a vmcnt(0) once per unrolled group.
 struct RegLayout {
   size_t ring, hist, row, total;
-  __host__ __device__ RegLayout(Variant v, int W, int T, int U, bool hist_lds, bool staged) {
+  __host__ __device__ RegLayout(Variant v, int W, int T, int U, bool hist_lds, bool staged,
+                                bool whole) {
     ring = 512;                                              // 64 sort keys (u64)
-    hist = ring + (size_t)kRing * kChunk * W * 4;
+    hist = ring + (size_t)kRing * (whole ? T : kChunk) * W * 4;
     const int nh = v == Variant::V2 ? 3 : 2;
     row = hist + (hist_lds ? (size_t)nh * T * W * 4 : 0);
-    total = row + ((v == Variant::V1 && staged) ? (size_t)U * 2 * 4 : 0);
+    // the staged v1 row: 64 * kV1Regs floats, so every lane stores all its registers without a
+    // branch (a branch around the store merges the wait counts into a vmcnt(0))
+    total = row + ((v == Variant::V1 && staged) ? (size_t)64 * kV1Regs * 4 : 0);
   }
 };
 
 // NMAX: a compile-time bound on n (8, 16, 32 or 64): the rank loop is unrolled to NMAX so its
 // broadcast key reads are issued back to back instead of one LDS round trip per pair.
-template <Variant V, bool STAGED, int NMAX>
+template <Variant V, bool STAGED, int NMAX, bool WHOLE>
 __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kV1 = V == Variant::V1, kV2 = V == Variant::V2;
@@ -60,10 +68,10 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   const int W = a.W, T = a.T, U = a.U;
   const int C = kV1 ? 2 : a.C;
   const int n = W * C;
-  const RegLayout L(V, W, T, U, hist_lds != 0, STAGED);
+  const RegLayout L(V, W, T, U, hist_lds != 0, STAGED, WHOLE);
   u64* keys = reinterpret_cast<u64*>(smem);
   int* ring = reinterpret_cast<int*>(smem + L.ring);
-  const int RW = kChunk * W;
+  const int RW = (WHOLE ? T : kChunk) * W;
   int* r_pred = ring;
   float* r_lp = reinterpret_cast<float*>(ring + RW);
   int* r_nt = ring + 2 * RW;
@@ -132,9 +140,8 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
 #pragma unroll
       for (int q = 0; q < R; ++q) {
         const int idx = lane + 64 * q;
-        if (idx < row_len) rowbuf[idx] = row[q];
+        rowbuf[idx] = row[q];  // (entries past 2U: never read)
       }
-      load_row(s + kAhead, row);
       lds_order();
     }
     // ---- candidate of this lane (decode_dev.h gen_candidate, one lane per candidate)
@@ -176,7 +183,6 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       valid = ok; code = i; lp = hist + row[0];
       nt = f ? bt : bt + 1; nu = f ? bu : bu + 1; fin = f;
     }
-    if constexpr (!kV1) load_row(s + kAhead, row);
     valid = valid && is_cand;
     // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
     const u64 key = ((u64)(valid ? lp_key(lp) : 0u) << 32) | (unsigned)(63 - lane);
@@ -235,7 +241,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     bfin = (g_pk >> 7) & 1;
     btot = g_tot;
     // ---- outputs of slot w (src/lib.rs:138-145), staged
-    const int cs = s % kChunk;
+    const int cs = WHOLE ? s : s % kChunk;
     if (is_cand && i == 0) {
       const int pc = g_pk & 0x7f;
       const int pred = pc == C ? sid : pc;
@@ -251,20 +257,27 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
         if constexpr (kV2) h_tot[hs] = btot;
       }
     }
-    if (cs == kChunk - 1 || s == T - 1) flush(s - cs, cs + 1);
+    if constexpr (!WHOLE) {
+      if (cs == kChunk - 1 || s == T - 1) flush(s - cs, cs + 1);
+    }
     return true;
   };
 
   bool ok = true;
   for (int s0 = 0; s0 < T && ok; s0 += kAhead) {  // unrolled by the ring: register indices fixed
 #pragma unroll
-    for (int k = 0; k < kAhead; ++k)
+    for (int k = 0; k < kAhead; ++k) {
       if (ok && s0 + k < T) ok = step(s0 + k, pre[k]);
+      // the refill is unconditional (clamped rows past T): a load skipped on some path would
+      // make the wait for the next row a vmcnt(0)
+      if constexpr (!kV1 || STAGED) load_row(s0 + k + kAhead, pre[k]);
+    }
   }
   if (!ok) {
     if (lane == 0 && a.status) atomicOr(a.status, kStatusNoCandidate);
     return;
   }
+  if constexpr (WHOLE) flush(0, T);
   if (!hist_lds) return;  // the host runs k_fused_paths over the global outputs
   // ---- backtrace of final slot `lane` (v2_util.rs:6-36 with final_branch = [0..W); util.rs:20-33
   // for slot 0 with t history = next_t)
@@ -426,21 +439,27 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
   int rc = SSNT_OK;
   if (n <= 64) {
     const bool staged = V != Variant::V1 || 2 * (size_t)a.U <= 64 * (size_t)kV1Regs;
-    const bool hist_lds = RegLayout(V, a.W, a.T, a.U, true, staged).total <= kMaxLds;
-    const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged).total;
+    const bool whole = RegLayout(V, a.W, a.T, a.U, true, staged, true).total <= kMaxLds;
+    const bool hist_lds = whole || RegLayout(V, a.W, a.T, a.U, true, staged, false).total <= kMaxLds;
+    const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged, whole).total;
     if (lds > kMaxLds) return SSNT_ERR_UNSUPPORTED;
     const int h = hist_lds ? 1 : 0;
-    if (!staged) {  // only v1 rows can be too long to stage
-      if constexpr (V == Variant::V1) rc = launch_with_lds(k_fused_reg<V, false, 64>, lds, a.B, st, a, h);
-    } else if (n <= 8) {
-      rc = launch_with_lds(k_fused_reg<V, true, 8>, lds, a.B, st, a, h);
-    } else if (n <= 16) {
-      rc = launch_with_lds(k_fused_reg<V, true, 16>, lds, a.B, st, a, h);
-    } else if (n <= 32) {
-      rc = launch_with_lds(k_fused_reg<V, true, 32>, lds, a.B, st, a, h);
-    } else {
-      rc = launch_with_lds(k_fused_reg<V, true, 64>, lds, a.B, st, a, h);
-    }
+    auto go = [&](auto kw, auto kc) {  // (NMAX, WHOLE) instance
+      constexpr int NM = decltype(kw)::value;
+      constexpr bool WH = decltype(kc)::value;
+      if (!staged) {  // only v1 rows can be too long to stage
+        if constexpr (V == Variant::V1) return launch_with_lds(k_fused_reg<V, false, 64, WH>, lds, a.B, st, a, h);
+        return (int)SSNT_ERR_UNSUPPORTED;
+      }
+      return launch_with_lds(k_fused_reg<V, true, NM, WH>, lds, a.B, st, a, h);
+    };
+    auto pick = [&](auto kc) {
+      if (n <= 8) return go(std::integral_constant<int, 8>{}, kc);
+      if (n <= 16) return go(std::integral_constant<int, 16>{}, kc);
+      if (n <= 32) return go(std::integral_constant<int, 32>{}, kc);
+      return go(std::integral_constant<int, 64>{}, kc);
+    };
+    rc = whole ? pick(std::true_type{}) : pick(std::false_type{});
     paths_kernel = want_paths && !hist_lds;
   } else {
     const size_t lds = (size_t)n * sizeof(Cand) + 2 * (size_t)n * 4 + (size_t)a.W * 2 * 16 +
