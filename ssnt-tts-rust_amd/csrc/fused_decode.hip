@@ -145,24 +145,25 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       lds_order();
     }
     // ---- candidate of this lane (decode_dev.h gen_candidate, one lane per candidate)
+    // straight-line selects, no exec-mask branches (each branch costs exec save/restore and
+    // splits the wait counts)
     const bool defined = !bfin && as_usize(bt) < I;
     int valid, code, nt, nu, fin, tot = btot;
     float lp;
-    if (!defined) {  // "End of input. Return values to fill padding region."
-      valid = i == 0; code = scode; lp = hist; nt = bt; nu = bu; fin = 1;
-    } else if constexpr (kV1) {  // src/lib.rs:186-227
-      const bool hdef = (unsigned)bu < (unsigned)T && (unsigned)bt < (unsigned)U;
-      float hv = 0.0f;
-      if (is_cand && hdef) {
-        if constexpr (STAGED) hv = rowbuf[2 * bt + i];  // bu == s for every live beam
-        else hv = src[((size_t)bu * U + bt) * 2 + i];
-      }
+    if constexpr (kV1) {  // src/lib.rs:186-227
+      const bool hdef = is_cand && (unsigned)bu < (unsigned)T && (unsigned)bt < (unsigned)U;
+      float hv;
+      if constexpr (STAGED) hv = rowbuf[hdef ? 2 * bt + i : 0];  // bu == s for every live beam
+      else hv = src[hdef ? ((size_t)bu * U + bt) * 2 + i : 0];
+      hv = hdef ? hv : 0.0f;
       const bool last = as_usize(bt) == I - 1;
+      const bool shift = i == 1;
       valid = 1;
-      if (i == 0 && last) { code = 0; lp = hist + hv; nt = bt; nu = bu; fin = 1; }
-      else if (i == 1 && last) { code = 0; lp = hist; nt = bt; nu = bu; fin = 1; }  // prohibited shift
-      else if (i == 1) { code = 1; lp = hist + hv; nt = bt + 1; nu = bu + 1; fin = 0; }
-      else { code = 0; lp = hist + hv; nt = bt; nu = bu + 1; fin = 0; }
+      code = (shift && !last) ? 1 : 0;
+      lp = (shift && last) ? hist : hist + hv;  // the prohibited last shift keeps the history
+      nt = (shift && !last) ? bt + 1 : bt;
+      nu = last ? bu : bu + 1;
+      fin = last ? 1 : 0;
     } else if constexpr (V == Variant::Tone) {  // src/tone_latent.rs:87-93, 220-231
       valid = 1; code = i; lp = hist + row[0]; nt = bt + 1; nu = bu + 1; fin = 0;
     } else {  // v2: src/v2.rs:119-166, 326-336
@@ -172,17 +173,22 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       const int lb = f2i_sat(fmaxf(diagonal - lower_range, 0.0f));
       const int ub = f2i_sat(fminf(diagonal + upper_range, (float)O));
       const bool overrun = (I - (t + 1)) * 3 > O;
-      bool f = false, ok = true;
-      if (!a.test_mode && (tot < lb || tot > ub)) ok = false;
-      else if (!a.test_mode && overrun) ok = false;
-      else if (t == I - 1) {
-        if (!a.test_mode && tot != (int)O) ok = false;
-        else if (!a.allow_skip && i == sid) ok = false;
-        else f = true;
-      } else if (!a.allow_skip && i == sid) ok = false;
+      const bool last = t == I - 1;
+      // the else-if chain of decode_beam_at as one conjunction
+      const bool ok = (a.test_mode || (tot >= lb && tot <= ub)) && (a.test_mode || !overrun) &&
+                      (!last || a.test_mode || tot == (int)O) && (a.allow_skip || i != sid);
+      const bool f = ok && last;
       valid = ok; code = i; lp = hist + row[0];
       nt = f ? bt : bt + 1; nu = f ? bu : bu + 1; fin = f;
     }
+    // "End of input. Return values to fill padding region." (src/lib.rs:57-67 etc.)
+    valid = defined ? valid : (i == 0);
+    code = defined ? code : scode;
+    lp = defined ? lp : hist;
+    nt = defined ? nt : bt;
+    nu = defined ? nu : bu;
+    fin = defined ? fin : 1;
+    tot = defined ? tot : btot;
     valid = valid && is_cand;
     // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
     const u64 key = ((u64)(valid ? lp_key(lp) : 0u) << 32) | (unsigned)(63 - lane);
