@@ -35,6 +35,23 @@ constexpr int kV1Regs = 4;   // v1 lattice row floats per lane: the row is stage
 constexpr int kChunk = 32;   // per-step outputs staged in LDS and flushed every kChunk steps
 constexpr int kRing = 7;     // staged output arrays
 
+// lane of the k-th set bit (k from 0) of a mask whose bits all lie below NMAX: a binary search
+// on popcounts -- replaces the compaction permute and one bpermute (two LDS round trips)
+template <int NMAX>
+__device__ __forceinline__ int kth_set_bit(u64 m, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int half = NMAX / 2; half >= 1; half >>= 1) {
+    const u64 low = half >= 64 ? ~0ull : ((1ull << half) - 1ull);
+    const int c = __popcll(m & low);
+    const bool up = k >= c;
+    k -= up ? c : 0;
+    pos += up ? half : 0;
+    m = up ? (m >> half) : m;
+  }
+  return pos;
+}
+
 // One wave per workgroup: LDS operations of a wave complete in order, so a write followed by a
 // read of the same location needs no barrier -- only the compiler must keep the order.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
@@ -235,10 +252,14 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       }
     }
     // ---- compaction (kept element k -> its sorted lane) and the cyclic pad
-    const int cdst = keep ? __popcll(kmask & below) : nkept + __popcll(~kmask & below);
-    const int kl = perm_i(cdst, lane);
     const int k = (dk >= 0 && w == W - 1) ? dk : (w < nkept ? w : w % nkept);
-    const int srcl = bperm_i(k, kl);
+    int srcl;  // sorted lane of kept element k
+    if constexpr (NMAX <= 16) {
+      srcl = kth_set_bit<NMAX>(kmask, k);
+    } else {  // (wider masks: the search costs more than the permute round trip it saves)
+      const int cdst = keep ? __popcll(kmask & below) : nkept + __popcll(~kmask & below);
+      srcl = bperm_i(k, perm_i(cdst, lane));
+    }
     const int g_lp = bperm_i(srcl, s_lp), g_ntu = bperm_i(srcl, s_ntu), g_pk = bperm_i(srcl, s_pk);
     const int g_tot = kV2 ? bperm_i(srcl, s_tot) : 0;
     hist = __int_as_float(g_lp);
