@@ -32,10 +32,10 @@ __device__ __forceinline__ int f2i_sat(float x) {
 // and +0 share a key, extended to a total order by placing NaN below -inf. NaN inputs are
 // outside the parity contract; the total order only guarantees that ranks are
 // a permutation (every output stays in range). Never 0: 0 marks "no candidate".
-__device__ __forceinline__ unsigned lp_key(float x) {
-  if (x != x) return 1u;
+__device__ __forceinline__ unsigned lp_key(float x) {  // selects only: no exec-mask branch
   const unsigned bits = x == 0.0f ? 0u : __float_as_uint(x);
-  return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+  const unsigned key = (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+  return x != x ? 1u : key;
 }
 
 __device__ __forceinline__ bool cand_eq(const Cand& a, const Cand& b, bool with_tot) {

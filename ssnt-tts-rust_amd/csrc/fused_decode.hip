@@ -208,7 +208,8 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     tot = defined ? tot : btot;
     valid = valid && is_cand;
     // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
-    const u64 key = ((u64)(valid ? lp_key(lp) : 0u) << 32) | (unsigned)(63 - lane);
+    const unsigned khi = lp_key(lp);
+    const u64 key = ((u64)(valid ? khi : 0u) << 32) | (unsigned)(63 - lane);
     keys[lane] = key;
     lds_order();
     int rank = 0;
