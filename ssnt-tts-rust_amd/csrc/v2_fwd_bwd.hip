@@ -90,19 +90,21 @@ __device__ __forceinline__ void f4_log_row(float* dst, const xf* row, int lo, in
 // pairwise tree (depth log2 DC instead of a DC-long add chain).
 template <bool FWD, int DC>
 __device__ __forceinline__ xf f4_cell(int x, const int* dur, const xf* w, const xf* src, int slo,
-                                      int shi) {
+                                      unsigned span, int zc) {
+  // source window [slo, slo + span] (an empty window comes as slo far above every total, so
+  // every offset is "negative", i.e. huge unsigned); out-of-window terms read the row buffer's
+  // always-zero cell zc: an exact zero term, as the oracle's skip
   float m[DC];
   int e[DC];
   int em = XF_EZERO;
-  const unsigned span = (unsigned)(shi - slo);  // (an empty window: every term out)
+  const int xr = x - slo;
 #pragma unroll
   for (int i = 0; i < DC; ++i) {
-    const unsigned yr = (unsigned)((FWD ? x - dur[i] : x + dur[i]) - slo);
-    const bool in = shi >= slo && yr <= span;
-    const xf v = src[in ? yr : 0];
+    const unsigned yr = (unsigned)(FWD ? xr - dur[i] : xr + dur[i]);
+    const xf v = src[yr <= span ? (int)yr : zc];
     const xf ww = w[i];
-    m[i] = in ? (FWD ? v.m * ww.m : ww.m * v.m) : 0.0f;
-    e[i] = in ? v.e + ww.e : XF_EZERO;
+    m[i] = FWD ? v.m * ww.m : ww.m * v.m;
+    e[i] = v.e + ww.e;
     em = max(em, e[i]);
   }
 #pragma unroll
@@ -186,7 +188,8 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
   constexpr int Dp = DC;  // class slots padded to DC (zero weight, duration 0)
   int* dur = reinterpret_cast<int*>(smem);
   xf* wbuf = reinterpret_cast<xf*>(smem + ((Dp * 4 + 15) & ~15));  // [2][Dp]
-  xf* row = wbuf + 2 * Dp;                                            // [2][Wc]
+  xf* row = wbuf + 2 * Dp;                                            // [2][Wc + 1]
+  const int RS = Wc + 1;  // row buffer stride: cell Wc is always zero
   const float* lg = a.logits + (size_t)b * Imax * D;
   const size_t drow = (size_t)(Imax + 1) * X;
   float* la = a.log_alpha ? a.log_alpha + b * drow : nullptr;
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
   // per chunk, none inside a step: a load consumed inside the step loop would make every step
   // wait for the ring stores before it, vmcnt counting both)
   constexpr int CH = 64;  // = a.chunk
-  float* chunk = reinterpret_cast<float*>(row + 2 * Wc);  // [2][CH][D]
+  float* chunk = reinterpret_cast<float*>(row + 2 * RS);  // [2][CH][D]
   auto st = [&](int k) { return fwd ? k : I - 1 - k; };  // input step of sweep step k
   auto stage = [&](int c) {  // chunk c = sweep steps [c*CH, (c+1)*CH)
     float* dstc = chunk + (c & 1) * CH * D;
@@ -241,6 +244,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
     if (tid == 0 && a.status) atomicOr(a.status, kStatusBadLength);
     return;
   }
+  if (tid < 2) row[tid * RS + Wc] = xf_zero();  // the always-zero cells
   for (int k = tid; k <= phi - plo; k += kF4Threads) {
     row[k] = xf{0.5f, 1};
     ws[(size_t)(fwd ? 0 : I) * Wc + k] = xf{0.5f, 1};
@@ -261,12 +265,15 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
     if ((k & 63) == 0) stage((k >> 6) + 1);  // first read CH = 64 steps (barriers) from now
     if (k < I) weights(k);                     // for the next iteration
     const xf* w = wbuf + ((k - 1) & 1) * Dp;
-    const xf* src = row + ((k - 1) & 1) * Wc;
-    xf* dst = row + (k & 1) * Wc;
+    const xf* src = row + ((k - 1) & 1) * RS;
+    xf* dst = row + (k & 1) * RS;
+    const bool pe = phi >= plo;  // previous window non-empty
+    const int slo = pe ? plo : (1 << 29);
+    const unsigned span = pe ? (unsigned)(phi - plo) : 0u;
     xf* wrow = ws + (size_t)r * Wc;
     for (int x = lo + tid; x <= hi; x += kF4Threads) {
-      const xf v = fwd ? f4_cell<true, DC>(x, dr, w, src, plo, phi)
-                       : f4_cell<false, DC>(x, dr, w, src, plo, phi);
+      const xf v = fwd ? f4_cell<true, DC>(x, dr, w, src, slo, span, Wc)
+                       : f4_cell<false, DC>(x, dr, w, src, slo, span, Wc);
       dst[x - lo] = v;
       wrow[x - lo] = v;
     }
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
   // Z over window(I): lane partials x mod 64, butterfly
   if (wave == 0) {
     xf acc = xf_zero();
-    const xf* rI = row + (I & 1) * Wc;
+    const xf* rI = row + (I & 1) * RS;
     for (int x = plo + ((lane - plo) & 63); x <= phi; x += 64) acc = f4_add(acc, rI[x - plo]);
     acc = f4_butterfly(acc);
     if (lane == 0) {
@@ -409,7 +416,7 @@ int launch_v2_fwd_bwd(const V2FwdBwdArgs& in, hipStream_t st) {
   const int Dp = a.D <= 8 ? 8 : a.D <= 16 ? 16 : a.D <= 32 ? 32 : 64;  // = DC
   const size_t head = (size_t)((Dp * 4 + 15) & ~15);
   a.chunk = 64;  // sweep steps per staged chunk (a power of two)
-  const size_t lds = head + 2 * (size_t)Dp * sizeof(xf) + 2 * (size_t)a.Wcap * sizeof(xf) +
+  const size_t lds = head + 2 * (size_t)Dp * sizeof(xf) + 2 * ((size_t)a.Wcap + 1) * sizeof(xf) +
                      2 * (size_t)a.chunk * a.D * sizeof(float);
   const size_t glds = head + 2 * (size_t)a.Wcap * sizeof(xf);
   if (lds > 160 * 1024 - 1024 || glds > 160 * 1024 - 1024) return SSNT_ERR_UNSUPPORTED;
