@@ -309,8 +309,8 @@ __global__ __launch_bounds__(kF4GradThreads) void k_f4_grad(V2FwdBwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int D = a.D, X = a.X, Imax = a.Imax, Wc = a.Wcap;
   int* dur = reinterpret_cast<int*>(smem);
-  xf* at = reinterpret_cast<xf*>(smem + ((D * 4 + 15) & ~15));  // alpha row t
-  xf* bn = at + Wc;                                                 // beta row t+1
+  xf* at = reinterpret_cast<xf*>(smem + ((D * 4 + 15) & ~15));  // alpha row t (+ zero cell Wc)
+  xf* bn = at + Wc + 1;                                             // beta row t+1
   float* g = a.grad ? a.grad + ((size_t)b * Imax + (t < Imax ? t : 0)) * D : nullptr;
   float* lb = a.log_beta ? a.log_beta + ((size_t)b * (Imax + 1) + t) * X : nullptr;
   const F4Ws W = f4_ws(a);
@@ -338,10 +338,13 @@ __global__ __launch_bounds__(kF4GradThreads) void k_f4_grad(V2FwdBwdArgs a) {
   const xf* ga = W.alpha + ((size_t)b * (Imax + 1) + t) * Wc;
   const xf* gb = W.beta + ((size_t)b * (Imax + 1) + t + 1) * Wc;
   for (int k = tid; k <= hi - lo; k += kF4GradThreads) at[k] = ga[k];
+  if (tid == 0) at[Wc] = xf_zero();
   for (int k = tid; k <= nhi - nlo; k += kF4GradThreads) bn[k] = gb[k];
   lds_sync();
   const float izm = 1.0f / Z.m;
   const int ize = -Z.e;
+  const unsigned span = hi >= lo ? (unsigned)(hi - lo) : 0u;
+  if (hi < lo) lo = 1 << 29;  // empty alpha window: every offset out of range
   auto emit = [&](int i, xf acc) {
     const xf S = f4_butterfly(acc);
     if (lane == 0) {
@@ -364,10 +367,9 @@ __global__ __launch_bounds__(kF4GradThreads) void k_f4_grad(V2FwdBwdArgs a) {
     for (int j = 0; j < NCW; ++j) {
       // a term outside the window is an exact zero: adding it leaves a normalized (or zero)
       // partial unchanged, so the select is the oracle's skip
-      const int y = x - di[j];
-      const bool in = y >= lo && y <= hi;
-      const xf av = at[in ? y - lo : 0];
-      acc[j] = xf_add(acc[j].m, acc[j].e, in ? av.m * bv.m : 0.0f, in ? av.e + bv.e : XF_EZERO);
+      const unsigned yr = (unsigned)(x - di[j] - lo);
+      const xf av = at[yr <= span ? (int)yr : Wc];  // (zero cell: the oracle's skip)
+      acc[j] = xf_add(acc[j].m, acc[j].e, av.m * bv.m, av.e + bv.e);
     }
   }
 #pragma unroll
@@ -418,7 +420,7 @@ int launch_v2_fwd_bwd(const V2FwdBwdArgs& in, hipStream_t st) {
   a.chunk = 64;  // sweep steps per staged chunk (a power of two)
   const size_t lds = head + 2 * (size_t)Dp * sizeof(xf) + 2 * ((size_t)a.Wcap + 1) * sizeof(xf) +
                      2 * (size_t)a.chunk * a.D * sizeof(float);
-  const size_t glds = head + 2 * (size_t)a.Wcap * sizeof(xf);
+  const size_t glds = head + (2 * (size_t)a.Wcap + 1) * sizeof(xf);
   if (lds > 160 * 1024 - 1024 || glds > 160 * 1024 - 1024) return SSNT_ERR_UNSUPPORTED;
   if (!a.workspace || a.workspace_bytes < v2_fwd_bwd_workspace_bytes(a.B, a.Imax, a.X - 1, a.test_mode))
     return SSNT_ERR_WORKSPACE;
