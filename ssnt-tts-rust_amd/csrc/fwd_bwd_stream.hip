@@ -118,6 +118,7 @@ __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 __device__ unsigned long long g_diag[1024][2 + 4 * kMaxW][8];
 struct Diag {
   unsigned long long t0 = __builtin_amdgcn_s_memtime(), wait = 0, cut = 0, cut_wait = 0;
+  unsigned long long ph[3] = {0, 0, 0};  // converters: cycles in convert (incl. load wait), ring write
   unsigned long long n = 0;
   __device__ unsigned long long now() const { return __builtin_amdgcn_s_memtime(); }
   __device__ void mark_cut() {
@@ -131,11 +132,15 @@ struct Diag {
       g_diag[b][w][2] = n;
       g_diag[b][w][3] = cut;
       g_diag[b][w][4] = cut_wait;
+      g_diag[b][w][5] = ph[0];
+      g_diag[b][w][6] = ph[1];
+      g_diag[b][w][7] = ph[2];
     }
   }
 };
 #else
 struct Diag {
+  unsigned long long ph[3] = {0, 0, 0};
   __device__ unsigned long long now() const { return 0; }
   __device__ void mark_cut() {}
   __device__ void flush(int, int) {}
@@ -708,8 +713,18 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
               O.m[j] = 1.0f; O.e[j] = 0;
             }
           } else {
+#ifdef SSNT_DIAG
+            const unsigned long long tl0 = dg.now();
+            asm volatile("" :: "v"(it.lt[0]), "v"(it.lt[2 * K - 1]));  // wait for the row here
+            const unsigned long long tc0 = dg.now();
+            dg.ph[2] += tc0 - tl0;
+#endif
             convert<K, OBS>(it, P, lane, E, Sh);
             convert_obs<K, OBS>(it, P, lane, O);
+#ifdef SSNT_DIAG
+            asm volatile("" :: "v"(E.m[0]), "v"(E.e[0]), "v"(Sh.m[K - 1]), "v"(Sh.e[K - 1]));
+            dg.ph[0] += dg.now() - tc0;
+#endif
           }
           XRow<K> Xs;
           if (d == 0) {  // L[p] = Sh[p-1]: canonical zero at p = 0
@@ -733,6 +748,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
               seen_grad = spin_until<true>([&] { return first_missing<kNH>(ctl->help[d], hb); }, q + 1, a.status, dg);
           }
           cbar();
+#ifdef SSNT_DIAG
+          const unsigned long long tw0 = dg.now();
+#endif
           unsigned char* sl = ring + (size_t)(r % R) * slot_bytes;
           float v[4 * K];
 #pragma unroll
@@ -756,6 +774,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           }
           cbar();
           ctr_st(&ctl->conv[d][c], k + 1);
+#ifdef SSNT_DIAG
+          dg.ph[1] += dg.now() - tw0;
+#endif
         }
         // refill after the old item is consumed: same registers, no copy (a copy of a register
         // with a load in flight would wait for the load)

@@ -46,5 +46,7 @@ for _ in range(5):
 print(f"exp={os.environ.get('SSNT_EXP', '0')} launch (incl. wrapper) median {np.median(times):.1f} us")
 for w, nm in enumerate(ROLES):
     tot, wait, nw, cut, cw = (np.median(d[:, w, i]) for i in range(5))
+    c0, c1, c2 = (np.median(d[:, w, i]) for i in (5, 6, 7))
+    extra = f"  load-wait {c2:7.0f} convert {c0:7.0f} ring-write {c1:7.0f}" if nm.startswith("conv") else ""
     print(f"{nm:12s} total {tot:8.0f}  spinning {wait:8.0f} ({nw:4.0f} spins)  cut@ {cut:8.0f}"
-          f" (spun {cw:7.0f} before)  per-step {tot / T:6.1f}")
+          f" (spun {cw:7.0f} before)  per-step {tot / T:6.1f}{extra}")
