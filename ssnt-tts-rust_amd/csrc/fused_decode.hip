@@ -68,9 +68,9 @@ struct RegLayout {
     hist = ring + (size_t)kRing * (whole ? T : kChunk) * W * 4;
     const int nh = v == Variant::V2 ? 3 : 2;
     row = hist + (hist_lds ? (size_t)nh * T * W * 4 : 0);
-    // the staged v1 row: 64 * kV1Regs floats, so every lane stores all its registers without a
-    // branch (a branch around the store merges the wait counts into a vmcnt(0))
-    total = row + ((v == Variant::V1 && staged) ? (size_t)64 * kV1Regs * 4 : 0);
+    // the staged v1 rows, double-buffered: 64 * kV1Regs floats each, so every lane stores all its
+    // registers without a branch (a branch around the store merges the wait counts into a vmcnt(0))
+    total = row + ((v == Variant::V1 && staged) ? (size_t)2 * 64 * kV1Regs * 4 : 0);
   }
 };
 
@@ -119,6 +119,10 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   // state of beam w, replicated in its C candidate lanes
   float hist = 0.0f;
   int bt = 0, bu = 0, bfin = 0, btot = 0;
+  // v1 staged: the two lattice values of beam w's next row at t = bt, read one step ahead by the
+  // candidate that became the beam and carried through the sort and the gather, so a step starts
+  // without an LDS round trip
+  float cv0 = 0.0f, cv1 = 0.0f;
 
   const int row_len = kV1 ? 2 * U : n;
   const float* src = a.src + (size_t)b * T * row_len;
@@ -133,6 +137,14 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   if constexpr (!kV1 || STAGED) {
 #pragma unroll
     for (int k = 0; k < kAhead; ++k) load_row(k, pre[k]);
+  }
+  if constexpr (kV1 && STAGED) {  // row 0 -> buffer 0; every beam starts at t = 0
+#pragma unroll
+    for (int q = 0; q < R; ++q) rowbuf[lane + 64 * q] = pre[0][q];
+    lds_order();
+    cv0 = rowbuf[0];
+    cv1 = rowbuf[1];
+    lds_order();
   }
 
   auto flush = [&](int s0, int steps) {  // staged outputs of steps [s0, s0+steps), coalesced
@@ -152,15 +164,14 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   };
 
   // one step; false when v2 finds no candidate (src/v2.rs:292)
-  auto step = [&](int s, float* row) -> bool {
-    if constexpr (kV1 && STAGED) {  // row s to LDS, then row s + kAhead into the freed registers
+  auto step = [&](int s, float* row, const float* nrow) -> bool {
+    float* nbuf = rowbuf + ((s + 1) & 1) * 64 * R;  // row s+1 (buffer last read by step s-1)
+    if constexpr (kV1 && STAGED) {
 #pragma unroll
-      for (int q = 0; q < R; ++q) {
-        const int idx = lane + 64 * q;
-        rowbuf[idx] = row[q];  // (entries past 2U: never read)
-      }
+      for (int q = 0; q < R; ++q) nbuf[lane + 64 * q] = nrow[q];  // (entries past 2U: never read)
       lds_order();
     }
+    (void)row;
     // ---- candidate of this lane (decode_dev.h gen_candidate, one lane per candidate)
     // straight-line selects, no exec-mask branches (each branch costs exec save/restore and
     // splits the wait counts)
@@ -170,7 +181,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     if constexpr (kV1) {  // src/lib.rs:186-227
       const bool hdef = is_cand && (unsigned)bu < (unsigned)T && (unsigned)bt < (unsigned)U;
       float hv;
-      if constexpr (STAGED) hv = rowbuf[hdef ? 2 * bt + i : 0];  // bu == s for every live beam
+      if constexpr (STAGED) hv = i == 0 ? cv0 : cv1;  // row s at t = bt (bu == s for every live beam)
       else hv = src[hdef ? ((size_t)bu * U + bt) * 2 + i : 0];
       hv = hdef ? hv : 0.0f;
       const bool last = as_usize(bt) == I - 1;
@@ -207,6 +218,13 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     fin = defined ? fin : 1;
     tot = defined ? tot : btot;
     valid = valid && is_cand;
+    // v1 staged: this candidate's row s+1 values at t = nt (read now, used by the next step)
+    float nv0 = 0.0f, nv1 = 0.0f;
+    if constexpr (kV1 && STAGED) {
+      const float2 v = *reinterpret_cast<const float2*>(nbuf + ((unsigned)nt < (unsigned)U ? 2 * nt : 0));
+      nv0 = v.x;
+      nv1 = v.y;
+    }
     // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
     const unsigned khi = lp_key(lp);
     const u64 key = ((u64)(valid ? khi : 0u) << 32) | (unsigned)(63 - lane);
@@ -231,6 +249,8 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     const int s_ntu = perm_i(dst, ntu);
     const int s_pk = perm_i(dst, pk);
     const int s_tot = kV2 ? perm_i(dst, tot) : 0;
+    const int s_v0 = (kV1 && STAGED) ? perm_i(dst, __float_as_int(nv0)) : 0;
+    const int s_v1 = (kV1 && STAGED) ? perm_i(dst, __float_as_int(nv1)) : 0;
     // ---- consecutive dedup, keep the first of each run (src/lib.rs:162; v2 adds the total)
     // every cross-lane read happens with the whole wave active: a DPP read of a lane that is
     // off in the exec mask returns the old value, so no shift may sit behind a short circuit
@@ -263,6 +283,10 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     }
     const int g_lp = bperm_i(srcl, s_lp), g_ntu = bperm_i(srcl, s_ntu), g_pk = bperm_i(srcl, s_pk);
     const int g_tot = kV2 ? bperm_i(srcl, s_tot) : 0;
+    if constexpr (kV1 && STAGED) {
+      cv0 = __int_as_float(bperm_i(srcl, s_v0));
+      cv1 = __int_as_float(bperm_i(srcl, s_v1));
+    }
     hist = __int_as_float(g_lp);
     bt = (int)((unsigned)g_ntu >> 16);
     bu = g_ntu & 0xffff;
@@ -295,7 +319,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   for (int s0 = 0; s0 < T && ok; s0 += kAhead) {  // unrolled by the ring: register indices fixed
 #pragma unroll
     for (int k = 0; k < kAhead; ++k) {
-      if (ok && s0 + k < T) ok = step(s0 + k, pre[k]);
+      if (ok && s0 + k < T) ok = step(s0 + k, pre[k], pre[(k + 1) % kAhead]);
       // the refill is unconditional (clamped rows past T): a load skipped on some path would
       // make the wait for the next row a vmcnt(0)
       if constexpr (!kV1 || STAGED) load_row(s0 + k + kAhead, pre[k]);
