@@ -33,7 +33,7 @@ using namespace dec;
 constexpr int kAhead = 4;    // input rows in flight
 constexpr int kV1Regs = 4;   // v1 lattice row floats per lane: the row is staged while 2U <= 256
 constexpr int kChunk = 32;   // per-step outputs staged in LDS and flushed every kChunk steps
-constexpr int kRing = 7;     // staged output arrays
+constexpr int kRec = 8;      // ints per staged output record (one per step and slot)
 
 // lane of the k-th set bit (k from 0) of a mask whose bits all lie below NMAX: a binary search
 // on popcounts -- replaces the compaction permute and one bpermute (two LDS round trips)
@@ -57,17 +57,20 @@ __device__ __forceinline__ int kth_set_bit(u64 m, int k) {
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
 // LDS layout of k_fused_reg (bytes), shared with the host launcher.
-// WHOLE: the staged outputs of all T steps fit, so they are flushed once after the loop -- no
-// global store inside the step loop, whose wait-count merge would otherwise turn the row
-// prefetch's wait into a vmcnt(0) once per unrolled group.
+// Staged outputs are records of kRec ints per (step, slot): {prediction, log_prob, next_t,
+// next_u | next_fin, parent slot, next_total, -}, two 16-byte stores per step.
+// WHOLE: the records of all T steps fit, so they are flushed once after the loop -- no global
+// store inside the step loop, whose wait-count merge would otherwise turn the row prefetch's
+// wait into a vmcnt(0) once per unrolled group -- and the backtrace reads them directly (no
+// separate history arrays).
 struct RegLayout {
   size_t ring, hist, row, total;
   __host__ __device__ RegLayout(Variant v, int W, int T, int U, bool hist_lds, bool staged,
                                 bool whole) {
     ring = 512;                                              // 64 sort keys (u64)
-    hist = ring + (size_t)kRing * (whole ? T : kChunk) * W * 4;
+    hist = ring + (size_t)kRec * (whole ? T : kChunk) * W * 4;
     const int nh = v == Variant::V2 ? 3 : 2;
-    row = hist + (hist_lds ? (size_t)nh * T * W * 4 : 0);
+    row = hist + ((hist_lds && !whole) ? (size_t)nh * T * W * 4 : 0);
     // the staged v1 rows, double-buffered: 64 * kV1Regs floats each, so every lane stores all its
     // registers without a branch (a branch around the store merges the wait counts into a vmcnt(0))
     total = row + ((v == Variant::V1 && staged) ? (size_t)2 * 64 * kV1Regs * 4 : 0);
@@ -87,16 +90,8 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   const int n = W * C;
   const RegLayout L(V, W, T, U, hist_lds != 0, STAGED, WHOLE);
   u64* keys = reinterpret_cast<u64*>(smem);
-  int* ring = reinterpret_cast<int*>(smem + L.ring);
-  const int RW = (WHOLE ? T : kChunk) * W;
-  int* r_pred = ring;
-  float* r_lp = reinterpret_cast<float*>(ring + RW);
-  int* r_nt = ring + 2 * RW;
-  int* r_nu = ring + 3 * RW;
-  int* r_fin = ring + 4 * RW;
-  int* r_tot = ring + 5 * RW;
-  int* r_br = ring + 6 * RW;
-  int* h_br = reinterpret_cast<int*>(smem + L.hist);  // (T,W) parent slot
+  int4* rec = reinterpret_cast<int4*>(smem + L.ring);  // 2 x int4 per (step, slot)
+  int* h_br = reinterpret_cast<int*>(smem + L.hist);  // (T,W) parent slot (!WHOLE)
   int* h_aux = h_br + (size_t)T * W;                   // (T,W) v1: next_t; v2/tone: prediction
   int* h_tot = h_aux + (size_t)T * W;                  // (T,W) v2: next_total_duration
   float* rowbuf = reinterpret_cast<float*>(smem + L.row);
@@ -152,13 +147,14 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     const int cnt = steps * W;
     const size_t g0 = ((size_t)b * T + s0) * W;
     for (int k = lane; k < cnt; k += 64) {
-      a.prediction[g0 + k] = r_pred[k];
-      a.log_prob[g0 + k] = r_lp[k];
-      a.next_t[g0 + k] = r_nt[k];
-      a.next_u[g0 + k] = r_nu[k];
-      a.next_fin[g0 + k] = r_fin[k] != 0;
-      a.beam_branch[g0 + k] = r_br[k];
-      if constexpr (kV2) a.next_total[g0 + k] = r_tot[k];
+      const int4 r0 = rec[2 * k], r1 = rec[2 * k + 1];
+      a.prediction[g0 + k] = r0.x;
+      a.log_prob[g0 + k] = __int_as_float(r0.y);
+      a.next_t[g0 + k] = r0.z;
+      a.next_u[g0 + k] = r0.w & 0x7fffffff;
+      a.next_fin[g0 + k] = r0.w < 0;
+      a.beam_branch[g0 + k] = r1.x;
+      if constexpr (kV2) a.next_total[g0 + k] = r1.y;
     }
     lds_order();
   };
@@ -299,10 +295,9 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       const int pred = pc == C ? sid : pc;
       const int parent = g_pk >> 8;
       const int o = cs * W + w;
-      r_pred[o] = pred; r_lp[o] = hist; r_nt[o] = bt; r_nu[o] = bu; r_fin[o] = bfin;
-      r_br[o] = parent;
-      if constexpr (kV2) r_tot[o] = btot;
-      if (hist_lds) {
+      rec[2 * o] = make_int4(pred, __float_as_int(hist), bt, (int)(((unsigned)bu & 0x7fffffffu) | ((unsigned)bfin << 31)));
+      rec[2 * o + 1] = make_int4(parent, kV2 ? btot : 0, 0, 0);
+      if (!WHOLE && hist_lds) {
         const int hs = s * W + w;
         h_br[hs] = parent;
         h_aux[hs] = kV1 ? bt : pred;
@@ -340,19 +335,37 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     int* pp = a.path_pred ? a.path_pred + ((size_t)b * W + lane) * T : nullptr;
     int* du = a.duration ? a.duration + ((size_t)b * W + lane) * T : nullptr;
     const bool best = lane == 0 && a.best_beam_branch;
+    // history of (s, slot): parent, aux (v1: next_t; v2/tone: prediction), next_total
+    auto hist_at = [&](int hs, int& parent, int& aux, int& tot) {
+      if constexpr (WHOLE) {
+        const int4 r0 = rec[2 * hs], r1 = rec[2 * hs + 1];
+        parent = r1.x;
+        aux = kV1 ? r0.z : r0.x;
+        tot = r1.y;
+      } else {
+        parent = h_br[hs];
+        aux = h_aux[hs];
+        tot = kV2 ? h_tot[hs] : 0;
+      }
+    };
     for (int s = T - 1; s >= 0; --s) {
       const int hs = s * W + cur;
-      const int parent = h_br[hs];
+      int parent, aux, tot;
+      hist_at(hs, parent, aux, tot);
       if (ord) ord[s] = cur;
       if constexpr (!kV1) {
-        if (pp) pp[s] = h_aux[hs];
+        if (pp) pp[s] = aux;
       }
       if constexpr (kV2) {
-        if (du) du[s] = h_tot[hs] - (s > 0 ? h_tot[hs - W - cur + parent] : 0);
+        if (du) {
+          int pp_, pa_, ptot = 0;
+          if (s > 0) hist_at(hs - W - cur + parent, pp_, pa_, ptot);
+          du[s] = tot - ptot;
+        }
       }
       if (best) {
         a.best_beam_branch[(size_t)b * T + s] = cur;
-        a.best_t_history[(size_t)b * T + s] = h_aux[hs];
+        a.best_t_history[(size_t)b * T + s] = aux;
       }
       cur = parent;
     }
