@@ -23,6 +23,7 @@
 
 #include <type_traits>
 
+#include "buffer_ops.h"
 #include "decode_dev.h"
 
 namespace ssnt {
@@ -31,6 +32,11 @@ namespace {
 using namespace dec;
 
 constexpr int kAhead = 4;    // input rows in flight
+
+// buffer resource over [base, base + bytes): loads past the end return 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
 constexpr int kV1Regs = 4;   // v1 lattice row floats per lane: the row is staged while 2U <= 256
 constexpr int kChunk = 32;   // per-step outputs staged in LDS and flushed every kChunk steps
 constexpr int kRec = 8;      // ints per staged output record (one per step and slot)
@@ -123,11 +129,15 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   const float* src = a.src + (size_t)b * T * row_len;
   constexpr int R = kV1 ? kV1Regs : 1;
   float pre[kAhead][R];
-  // unconditional (clamped) loads: a conditional load becomes a branch whose join waits for it
+  // unconditional loads (a conditional load becomes a branch whose join waits for it) through a
+  // buffer resource over this utterance's rows: one lane offset, the row as the scalar offset,
+  // the register index as the immediate; entries past the row end are never read, and past the
+  // utterance the hardware returns 0
+  const __amdgpu_buffer_rsrc_t rows_rs = brsrc(src, (unsigned)((size_t)T * row_len * 4));
   auto load_row = [&](int s, float* dst) {
+    const int soff = min(s, T - 1) * row_len * 4;
 #pragma unroll
-    for (int q = 0; q < R; ++q)
-      dst[q] = src[(size_t)min(s, T - 1) * row_len + min(lane + 64 * q, row_len - 1)];
+    for (int q = 0; q < R; ++q) dst[q] = rbuf_ld1(rows_rs, 4 * lane + 256 * q, soff, 0);
   };
   if constexpr (!kV1 || STAGED) {
 #pragma unroll
@@ -314,10 +324,13 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   for (int s0 = 0; s0 < T && ok; s0 += kAhead) {  // unrolled by the ring: register indices fixed
 #pragma unroll
     for (int k = 0; k < kAhead; ++k) {
-      if (ok && s0 + k < T) ok = step(s0 + k, pre[k], pre[(k + 1) % kAhead]);
       // the refill is unconditional (clamped rows past T): a load skipped on some path would
-      // make the wait for the next row a vmcnt(0)
-      if constexpr (!kV1 || STAGED) load_row(s0 + k + kAhead, pre[k]);
+      // make the wait for the next row a vmcnt(0). v1 staged: step s reads only row s+1 (row s
+      // was staged by step s-1), so row s's registers are refilled before the step, ahead of
+      // its LDS traffic; the other variants read row s in the step and refill after it.
+      if constexpr (kV1 && STAGED) load_row(s0 + k + kAhead, pre[k]);
+      if (ok && s0 + k < T) ok = step(s0 + k, pre[k], pre[(k + 1) % kAhead]);
+      if constexpr (!kV1) load_row(s0 + k + kAhead, pre[k]);
     }
   }
   if (!ok) {
