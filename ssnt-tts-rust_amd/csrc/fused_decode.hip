@@ -8,7 +8,9 @@
 //   n <= 64  k_fused_reg: one candidate per lane; only the sort keys and the staged outputs touch
 //            LDS.
 //     rank     #{j : key_j > key_c} with key = (lp_key(lp), 63 - c): the stable descending sort
-//              of src/lib.rs:161 (ties keep generation order), over broadcast LDS reads
+//              of src/lib.rs:161 (ties keep generation order), over broadcast LDS reads; for
+//              n <= 8 the wave holds 8 replicas of the candidates and each lane does one of the
+//              64 pairwise compares (one bpermute, one ballot, a byte popcount)
 //     sort     ds_permute of the packed candidate fields to lane = rank
 //     dedup    compare with the DPP-shifted left neighbour (src/lib.rs:162, eq_ignore_parent)
 //     diagonal ballot of the kept on-diagonal lanes (src/v2.rs:283-308)
@@ -44,12 +46,14 @@ constexpr int kRec = 8;      // ints per staged output record (one per step and 
 // lane of the k-th set bit (k from 0) of a mask whose bits all lie below NMAX: a binary search
 // on popcounts -- replaces the compaction permute and one bpermute (two LDS round trips)
 template <int NMAX>
-__device__ __forceinline__ int kth_set_bit(u64 m, int k) {
+__device__ __forceinline__ int kth_set_bit(u64 m64, int k) {
+  static_assert(NMAX <= 32, "32-bit search");
+  unsigned m = (unsigned)m64;  // 32-bit shifts and popcounts (the 64-bit forms take two passes)
   int pos = 0;
 #pragma unroll
   for (int half = NMAX / 2; half >= 1; half >>= 1) {
-    const u64 low = half >= 64 ? ~0ull : ((1ull << half) - 1ull);
-    const int c = __popcll(m & low);
+    const unsigned low = (1u << half) - 1u;
+    const int c = __popc(m & low);
     const bool up = k >= c;
     k -= up ? c : 0;
     pos += up ? half : 0;
@@ -104,9 +108,17 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
 
   const u64 I = as_usize(a.input_length[b]);
   const u64 O = kV2 ? as_usize(a.output_length[b]) : 0;
-  const bool is_cand = lane < n;
-  const int w = is_cand ? lane / C : 0;  // the beam this lane expands (generation order w*C + i)
-  const int i = is_cand ? lane - w * C : 0;
+  // NMAX == 8: the wave holds 8 replicas of the candidate set (lane = 8 * replica + candidate), so
+  // the rank is one pairwise compare per lane and a byte popcount of its ballot, and every step
+  // below runs identically in each replica
+  constexpr bool kRep = NMAX == 8;
+  constexpr u64 kGrp = kRep ? 0xffull : ~0ull;  // ballot bits of replica 0
+  const int c = kRep ? (lane & 7) : lane;       // candidate index of this lane
+  const int gbase = kRep ? (lane & ~7) : 0;     // first lane of this lane's replica
+  const bool is_cand = c < n;
+  const int w = is_cand ? c / C : 0;  // the beam this lane expands (generation order w*C + i)
+  const int i = is_cand ? c - w * C : 0;
+  const bool writer = gbase == 0 && is_cand && i == 0;  // the lane that stages slot w's outputs
   const int sid = a.special_id;
   // prediction code: class index, or C for the "not defined" padding candidate whose prediction
   // is the special id (equal to class sid when sid names a class: eq_ignore_parent compares it)
@@ -137,7 +149,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   auto load_row = [&](int s, float* dst) {
     const int soff = min(s, T - 1) * row_len * 4;
 #pragma unroll
-    for (int q = 0; q < R; ++q) dst[q] = rbuf_ld1(rows_rs, 4 * lane + 256 * q, soff, 0);
+    for (int q = 0; q < R; ++q) dst[q] = rbuf_ld1(rows_rs, 4 * (kV1 ? lane : c) + 256 * q, soff, 0);
   };
   if constexpr (!kV1 || STAGED) {
 #pragma unroll
@@ -185,7 +197,8 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     int valid, code, nt, nu, fin, tot = btot;
     float lp;
     if constexpr (kV1) {  // src/lib.rs:186-227
-      const bool hdef = is_cand && (unsigned)bu < (unsigned)T && (unsigned)bt < (unsigned)U;
+      const bool hdef = ((is_cand ? 1 : 0) & ((unsigned)bu < (unsigned)T ? 1 : 0) &
+                         ((unsigned)bt < (unsigned)U ? 1 : 0)) != 0;  // bitwise: no branch
       float hv;
       if constexpr (STAGED) hv = i == 0 ? cv0 : cv1;  // row s at t = bt (bu == s for every live beam)
       else hv = src[hdef ? ((size_t)bu * U + bt) * 2 + i : 0];
@@ -233,22 +246,35 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     }
     // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
     const unsigned khi = lp_key(lp);
-    const u64 key = ((u64)(valid ? khi : 0u) << 32) | (unsigned)(63 - lane);
-    keys[lane] = key;
-    lds_order();
+    const u64 key = ((u64)(valid ? khi : 0u) << 32) | (unsigned)(63 - c);
     int rank = 0;
-    // keys of lanes >= n are below every valid key (their high word is 0): reading them is harmless
+    if constexpr (kRep) {
+      // lane 8x + y compares its candidate y with candidate x (read from lane x): bit 8x + y of
+      // the ballot says y sorts before x, so candidate x's rank is the popcount of byte x
+      const int xl = lane >> 3;
+      const unsigned klo = (unsigned)bperm_i(xl, (int)(unsigned)key);
+      const unsigned khx = (unsigned)bperm_i(xl, (int)(unsigned)(key >> 32));
+      const u64 beats = __ballot(key > (((u64)khx << 32) | klo));
+      rank = __popc((unsigned)(beats >> (8 * c)) & 0xffu);
+    } else {
+      keys[lane] = key;
+      lds_order();
+      // keys of lanes >= n are below every valid key (their high word is 0): reading them is harmless
 #pragma unroll
-    for (int j = 0; j < NMAX; j += 2) {
-      const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(keys + j);  // broadcast read
-      rank += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
+      for (int j = 0; j < NMAX; j += 2) {
+        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(keys + j);  // broadcast read
+        rank += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
+      }
+      lds_order();
     }
-    lds_order();
-    const u64 vmask = __ballot(valid);
+    const u64 vmask = __ballot(valid) & kGrp;
     const int nvalid = __popcll(vmask);
     const u64 below = (1ull << lane) - 1ull;
-    // a full permutation of the 64 lanes: valid candidates to their rank, the rest after them
-    const int dst = valid ? rank : nvalid + __popcll(~vmask & below);
+    // a full permutation of the 64 lanes: every key is distinct and the invalid ones (high word
+    // 0) lie below the valid ones, so the lanes < NMAX rank to [0, NMAX) -- valid candidates to
+    // [0, nvalid) -- and the lanes past the bound keep their place (replicas: within the replica)
+    const int dst = kRep ? (gbase | rank) : (lane < NMAX ? rank : lane);
+    const int sp = kRep ? (lane & 7) : lane;  // sorted position of this lane
     const int pk = code | (fin << 7) | (w << 8);
     const int ntu = (nt << 16) | (nu & 0xffff);
     const int s_lp = perm_i(dst, __float_as_int(lp));
@@ -264,8 +290,9 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     const int p_tot = kV2 ? wave_shr1(s_tot) : 0;
     const bool same = (((s_pk ^ p_pk) & 0xff) == 0) & (__int_as_float(s_lp) == __int_as_float(p_lp)) &
                       (s_ntu == p_ntu) & (s_tot == p_tot);
-    const bool keep = lane < nvalid && (lane == 0 || !same);
-    const u64 kmask = __ballot(keep);
+    // bitwise, not short-circuit: the && form compiles to an exec-mask branch around the compare
+    const bool keep = ((sp < nvalid ? 1 : 0) & ((sp == 0 ? 1 : 0) | (same ? 0 : 1))) != 0;
+    const u64 kmask = __ballot(keep) & kGrp;
     const int nkept = __popcll(kmask);
     if (nkept == 0) return false;  // v2 only: assert_ne!(n_results, 0) (src/v2.rs:292)
     // ---- v2 diagonal injection (src/v2.rs:283-308): first kept candidate on the diagonal
@@ -274,7 +301,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       if (!a.test_mode) {
         const float diag = o_over_i * (float)(u64)((unsigned)s_ntu >> 16);
         const float diff = (float)s_tot - diag;
-        const u64 dmask = __ballot(keep && diff >= -20.0f && diff <= 0.0f);
+        const u64 dmask = __ballot(keep && diff >= -20.0f && diff <= 0.0f) & kGrp;
         if (dmask) dk = __popcll(kmask & ((1ull << (__ffsll((long long)dmask) - 1)) - 1ull));
       }
     }
@@ -282,7 +309,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     const int k = (dk >= 0 && w == W - 1) ? dk : (w < nkept ? w : w % nkept);
     int srcl;  // sorted lane of kept element k
     if constexpr (NMAX <= 16) {
-      srcl = kth_set_bit<NMAX>(kmask, k);
+      srcl = gbase | kth_set_bit<NMAX>(kmask, k);
     } else {  // (wider masks: the search costs more than the permute round trip it saves)
       const int cdst = keep ? __popcll(kmask & below) : nkept + __popcll(~kmask & below);
       srcl = bperm_i(k, perm_i(cdst, lane));
@@ -300,13 +327,14 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     btot = g_tot;
     // ---- outputs of slot w (src/lib.rs:138-145), staged
     const int cs = WHOLE ? s : s % kChunk;
-    if (is_cand && i == 0) {
+    if (writer) {
       const int pc = g_pk & 0x7f;
       const int pred = pc == C ? sid : pc;
       const int parent = g_pk >> 8;
       const int o = cs * W + w;
       rec[2 * o] = make_int4(pred, __float_as_int(hist), bt, (int)(((unsigned)bu & 0x7fffffffu) | ((unsigned)bfin << 31)));
-      rec[2 * o + 1] = make_int4(parent, kV2 ? btot : 0, 0, 0);
+      if constexpr (kV2) rec[2 * o + 1] = make_int4(parent, btot, 0, 0);
+      else reinterpret_cast<int*>(rec + 2 * o + 1)[0] = parent;  // (y..w never read)
       if (!WHOLE && hist_lds) {
         const int hs = s * W + w;
         h_br[hs] = parent;
