@@ -62,6 +62,10 @@ __device__ __forceinline__ int kth_set_bit(u64 m64, int k) {
   return pos;
 }
 
+// ballot of a bool (HIP's __ballot takes an int, and the int -> bool compare costs a select and a
+// compare per call)
+__device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 // One wave per workgroup: LDS operations of a wave complete in order, so a write followed by a
 // read of the same location needs no barrier -- only the compiler must keep the order.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
@@ -254,7 +258,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       const int xl = lane >> 3;
       const unsigned klo = (unsigned)bperm_i(xl, (int)(unsigned)key);
       const unsigned khx = (unsigned)bperm_i(xl, (int)(unsigned)(key >> 32));
-      const u64 beats = __ballot(key > (((u64)khx << 32) | klo));
+      const u64 beats = ballot(key > (((u64)khx << 32) | klo));
       rank = __popc((unsigned)(beats >> (8 * c)) & 0xffu);
     } else {
       keys[lane] = key;
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       }
       lds_order();
     }
-    const u64 vmask = __ballot(valid) & kGrp;
+    const u64 vmask = ballot(valid != 0) & kGrp;
     const int nvalid = __popcll(vmask);
     const u64 below = (1ull << lane) - 1ull;
     // a full permutation of the 64 lanes: every key is distinct and the invalid ones (high word
@@ -292,21 +296,31 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
                       (s_ntu == p_ntu) & (s_tot == p_tot);
     // bitwise, not short-circuit: the && form compiles to an exec-mask branch around the compare
     const bool keep = ((sp < nvalid ? 1 : 0) & ((sp == 0 ? 1 : 0) | (same ? 0 : 1))) != 0;
-    const u64 kmask = __ballot(keep) & kGrp;
+    const u64 kmask = ballot(keep) & kGrp;
     const int nkept = __popcll(kmask);
-    if (nkept == 0) return false;  // v2 only: assert_ne!(n_results, 0) (src/v2.rs:292)
+    if constexpr (kV2) {  // assert_ne!(n_results, 0) (src/v2.rs:292); v1/tone always keep one
+      if (nkept == 0) return false;
+    }
     // ---- v2 diagonal injection (src/v2.rs:283-308): first kept candidate on the diagonal
     int dk = -1;
     if constexpr (kV2) {
       if (!a.test_mode) {
         const float diag = o_over_i * (float)(u64)((unsigned)s_ntu >> 16);
         const float diff = (float)s_tot - diag;
-        const u64 dmask = __ballot(keep && diff >= -20.0f && diff <= 0.0f) & kGrp;
+        const u64 dmask = ballot(keep && diff >= -20.0f && diff <= 0.0f) & kGrp;
         if (dmask) dk = __popcll(kmask & ((1ull << (__ffsll((long long)dmask) - 1)) - 1ull));
       }
     }
     // ---- compaction (kept element k -> its sorted lane) and the cyclic pad
-    const int k = (dk >= 0 && w == W - 1) ? dk : (w < nkept ? w : w % nkept);
+    int k;
+    if constexpr (kV1 && kRep) {  // w < W <= 4: w % nkept by three wrapping subtractions
+      unsigned kk = (unsigned)w;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) kk = min(kk, kk - (unsigned)nkept);
+      k = (int)kk;
+    } else {
+      k = (dk >= 0 && w == W - 1) ? dk : (w < nkept ? w : w % nkept);
+    }
     int srcl;  // sorted lane of kept element k
     if constexpr (NMAX <= 16) {
       srcl = gbase | kth_set_bit<NMAX>(kmask, k);

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# GPU box: configs[2] decode kernel time of the product library and each named var_* build,
+# GPU box: configs[2] (and configs[4] v2 / tone) decode kernel time of the product library and each named var_* build,
 # alternating, same box (rocprof kernel stats). Tuning study only.
 set -euo pipefail
 cd "$(dirname "$0")/.."
@@ -11,6 +11,8 @@ sys.path.insert(0, "tools")
 import bench_configs as bc
 bc.cpu_time = lambda f: 1.0
 print(json.dumps(bc.decode_config(256, 200, 80, 4, iters=50)))
+print(json.dumps(bc.v2_decode_config(64, 400, 2000, 16, 4, iters=10)))
+print(json.dumps(bc.tone_decode_config(64, 400, 5, 4, iters=10)))
 PY
 for n in prod "$@" prod "$@"; do
   if [ $n = prod ]; then unset SSNT_TTS_C_LIB; else export SSNT_TTS_C_LIB=$PWD/ssnt-tts-rust_amd/lib/var_$n/libssnt_tts_c.so; fi
@@ -20,6 +22,6 @@ for n in prod "$@" prod "$@"; do
 import csv
 for r in csv.DictReader(open('gpurun_out/prof_ab_$n/kt_kernel_stats.csv')):
     if 'fused' in r['Name']:
-        print('$n', r['Name'][50:100], r['Calls'], round(float(r['AverageNs'])/1e3, 2))
+        print('$n', r['Name'][50:110], r['Calls'], round(float(r['AverageNs'])/1e3, 2))
 "
 done
