@@ -90,18 +90,23 @@ __device__ __forceinline__ void f4_log_row(float* dst, const xf* row, int lo, in
 // pairwise tree (depth log2 DC instead of a DC-long add chain).
 template <bool FWD, int DC>
 __device__ __forceinline__ xf f4_cell(int x, const int* dur, const xf* w, const xf* src, int slo,
-                                      unsigned span, int zc) {
-  // source window [slo, slo + span] (an empty window comes as slo far above every total, so
-  // every offset is "negative", i.e. huge unsigned); out-of-window terms read the row buffer's
-  // always-zero cell zc: an exact zero term, as the oracle's skip
+                                      int span) {
+  // source window [slo, slo + span] (span = -1: empty). Offsets are taken +1, so everything left
+  // of the window is negative, i.e. huge unsigned, and one unsigned min clamps an out-of-window
+  // term onto the zero cell just right of the window (index span + 1), and offset 0 is the zero
+  // cell left of it (index -1): an exact zero term, as the oracle's skip
   float m[DC];
   int e[DC];
   int em = XF_EZERO;
-  const int xr = x - slo;
+  int xr1 = x - slo + 1;
+  // opaque: otherwise the compiler reassociates xr1 - dur[i] into x + (1 - slo - dur[i]) with
+  // the 2 DC uniform sums in SGPRs, which overflows the SGPR file into lane spills every step
+  asm volatile("" : "+v"(xr1));
+  const unsigned lim = (unsigned)(span + 2);
 #pragma unroll
   for (int i = 0; i < DC; ++i) {
-    const unsigned yr = (unsigned)(FWD ? xr - dur[i] : xr + dur[i]);
-    const xf v = src[yr <= span ? (int)yr : zc];
+    const unsigned yr1 = (unsigned)(FWD ? xr1 - dur[i] : xr1 + dur[i]);
+    const xf v = src[(int)min(yr1, lim) - 1];
     const xf ww = w[i];
     m[i] = FWD ? v.m * ww.m : ww.m * v.m;
     e[i] = v.e + ww.e;
@@ -188,8 +193,11 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
   constexpr int Dp = DC;  // class slots padded to DC (zero weight, duration 0)
   int* dur = reinterpret_cast<int*>(smem);
   xf* wbuf = reinterpret_cast<xf*>(smem + ((Dp * 4 + 15) & ~15));  // [2][Dp]
-  xf* row = wbuf + 2 * Dp;                                            // [2][Wc + 1]
-  const int RS = Wc + 1;  // row buffer stride: cell Wc is always zero
+  // row buffers [2][Wc + 3]: a zero cell, the window cells, a zero cell right after the window
+  // (rewritten every step), spare; rb(k) is buffer k's cell 0
+  xf* row = wbuf + 2 * Dp;
+  const int RS = Wc + 3;
+  auto rb = [&](int k) { return row + k * RS + 1; };
   const float* lg = a.logits + (size_t)b * Imax * D;
   const size_t drow = (size_t)(Imax + 1) * X;
   float* la = a.log_alpha ? a.log_alpha + b * drow : nullptr;
@@ -244,13 +252,14 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
     if (tid == 0 && a.status) atomicOr(a.status, kStatusBadLength);
     return;
   }
-  if (tid < 2) row[tid * RS + Wc] = xf_zero();  // the always-zero cells
+  if (tid < 2) rb(tid)[-1] = xf_zero();  // the always-zero cells left of each window
+  if (tid == 0) rb(0)[max(phi - plo + 1, 0)] = xf_zero();
   for (int k = tid; k <= phi - plo; k += kF4Threads) {
-    row[k] = xf{0.5f, 1};
+    rb(0)[k] = xf{0.5f, 1};
     ws[(size_t)(fwd ? 0 : I) * Wc + k] = xf{0.5f, 1};
   }
   lds_sync();
-  if (fwd && la) f4_log_row(la, row, 0, 0, X);
+  if (fwd && la) f4_log_row(la, rb(0), 0, 0, X);
   for (int k = 1; k <= I; ++k) {
     const int r = fwd ? k : I - k;  // row produced by this step
     int lo, hi;
@@ -265,18 +274,19 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
     if ((k & 63) == 0) stage((k >> 6) + 1);  // first read CH = 64 steps (barriers) from now
     if (k < I) weights(k);                     // for the next iteration
     const xf* w = wbuf + ((k - 1) & 1) * Dp;
-    const xf* src = row + ((k - 1) & 1) * RS;
-    xf* dst = row + (k & 1) * RS;
+    const xf* src = rb((k - 1) & 1);
+    xf* dst = rb(k & 1);
     const bool pe = phi >= plo;  // previous window non-empty
-    const int slo = pe ? plo : (1 << 29);
-    const unsigned span = pe ? (unsigned)(phi - plo) : 0u;
+    const int slo = pe ? plo : 0;
+    const int span = pe ? phi - plo : -1;
     xf* wrow = ws + (size_t)r * Wc;
     for (int x = lo + tid; x <= hi; x += kF4Threads) {
-      const xf v = fwd ? f4_cell<true, DC>(x, dr, w, src, slo, span, Wc)
-                       : f4_cell<false, DC>(x, dr, w, src, slo, span, Wc);
+      const xf v = fwd ? f4_cell<true, DC>(x, dr, w, src, slo, span)
+                       : f4_cell<false, DC>(x, dr, w, src, slo, span);
       dst[x - lo] = v;
       wrow[x - lo] = v;
     }
+    if (tid == kF4Threads - 1) dst[max(hi - lo + 1, 0)] = xf_zero();  // (no cell writes there)
     lds_sync();
     if (fwd && la) f4_log_row(la + (size_t)r * X, dst, lo, hi, X);
     plo = lo;
@@ -288,7 +298,7 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
   // Z over window(I): lane partials x mod 64, butterfly
   if (wave == 0) {
     xf acc = xf_zero();
-    const xf* rI = row + (I & 1) * RS;
+    const xf* rI = rb(I & 1);
     for (int x = plo + ((lane - plo) & 63); x <= phi; x += 64) acc = f4_add(acc, rI[x - plo]);
     acc = f4_butterfly(acc);
     if (lane == 0) {
@@ -418,7 +428,7 @@ int launch_v2_fwd_bwd(const V2FwdBwdArgs& in, hipStream_t st) {
   const int Dp = a.D <= 8 ? 8 : a.D <= 16 ? 16 : a.D <= 32 ? 32 : 64;  // = DC
   const size_t head = (size_t)((Dp * 4 + 15) & ~15);
   a.chunk = 64;  // sweep steps per staged chunk (a power of two)
-  const size_t lds = head + 2 * (size_t)Dp * sizeof(xf) + 2 * ((size_t)a.Wcap + 1) * sizeof(xf) +
+  const size_t lds = head + 2 * (size_t)Dp * sizeof(xf) + 2 * ((size_t)a.Wcap + 3) * sizeof(xf) +
                      2 * (size_t)a.chunk * a.D * sizeof(float);
   const size_t glds = head + (2 * (size_t)a.Wcap + 1) * sizeof(xf);
   if (lds > 160 * 1024 - 1024 || glds > 160 * 1024 - 1024) return SSNT_ERR_UNSUPPORTED;
