@@ -112,13 +112,16 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
 
   const u64 I = as_usize(a.input_length[b]);
   const u64 O = kV2 ? as_usize(a.output_length[b]) : 0;
-  // NMAX == 8: the wave holds 8 replicas of the candidate set (lane = 8 * replica + candidate), so
-  // the rank is one pairwise compare per lane and a byte popcount of its ballot, and every step
-  // below runs identically in each replica
-  constexpr bool kRep = NMAX == 8;
-  constexpr u64 kGrp = kRep ? 0xffull : ~0ull;  // ballot bits of replica 0
-  const int c = kRep ? (lane & 7) : lane;       // candidate index of this lane
-  const int gbase = kRep ? (lane & ~7) : 0;     // first lane of this lane's replica
+  // NMAX < 64: the wave holds 64 / NMAX replicas of the candidate set (lane = NMAX * replica +
+  // candidate); each replica does its share of the rank compares, and every later stage runs
+  // identically in each replica. NMAX == 8: the rank is one pairwise compare per lane and a byte
+  // popcount of its ballot; 16 / 32: partial counts summed across replicas by lane swaps.
+  constexpr bool kRep8 = NMAX == 8;
+  constexpr bool kRep = NMAX < 64;
+  constexpr int kReps = 64 / NMAX;
+  constexpr u64 kGrp = NMAX == 64 ? ~0ull : ((1ull << NMAX) - 1ull);  // ballot bits of replica 0
+  const int c = lane & (NMAX - 1);      // candidate index of this lane
+  const int gbase = lane & ~(NMAX - 1);  // first lane of this lane's replica
   const bool is_cand = c < n;
   const int w = is_cand ? c / C : 0;  // the beam this lane expands (generation order w*C + i)
   const int i = is_cand ? c - w * C : 0;
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     const unsigned khi = lp_key(lp);
     const u64 key = ((u64)(valid ? khi : 0u) << 32) | (unsigned)(63 - c);
     int rank = 0;
-    if constexpr (kRep) {
+    if constexpr (kRep8) {
       // lane 8x + y compares its candidate y with candidate x (read from lane x): bit 8x + y of
       // the ballot says y sorts before x, so candidate x's rank is the popcount of byte x
       const int xl = lane >> 3;
@@ -260,6 +263,26 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       const unsigned khx = (unsigned)bperm_i(xl, (int)(unsigned)(key >> 32));
       const u64 beats = ballot(key > (((u64)khx << 32) | klo));
       rank = __popc((unsigned)(beats >> (8 * c)) & 0xffu);
+    } else if constexpr (kRep) {
+      // replica r counts the keys [r JN, (r + 1) JN) of replica 0 that beat its candidate (reads
+      // broadcast within the replica); the partial counts are summed across replicas by swapping
+      // 16-lane rows and 32-lane halves
+      constexpr int JN = NMAX / kReps;
+      keys[lane] = key;
+      lds_order();
+      const u64* kr = keys + (lane / NMAX) * JN;
+#pragma unroll
+      for (int j = 0; j < JN; j += 2) {
+        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(kr + j);
+        rank += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
+      }
+      lds_order();
+      if constexpr (kReps == 4) {
+        const auto r16 = __builtin_amdgcn_permlane16_swap(rank, rank, false, false);
+        rank = (int)(r16[0] + r16[1]);
+      }
+      const auto r32 = __builtin_amdgcn_permlane32_swap(rank, rank, false, false);
+      rank = (int)(r32[0] + r32[1]);
     } else {
       keys[lane] = key;
       lds_order();
@@ -273,12 +296,12 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     }
     const u64 vmask = ballot(valid != 0) & kGrp;
     const int nvalid = __popcll(vmask);
-    const u64 below = (1ull << lane) - 1ull;
+    const u64 below = (1ull << c) - 1ull;  // candidates of this replica before this lane
     // a full permutation of the 64 lanes: every key is distinct and the invalid ones (high word
     // 0) lie below the valid ones, so the lanes < NMAX rank to [0, NMAX) -- valid candidates to
     // [0, nvalid) -- and the lanes past the bound keep their place (replicas: within the replica)
     const int dst = kRep ? (gbase | rank) : (lane < NMAX ? rank : lane);
-    const int sp = kRep ? (lane & 7) : lane;  // sorted position of this lane
+    const int sp = c;  // sorted position of this lane within its replica
     const int pk = code | (fin << 7) | (w << 8);
     const int ntu = (nt << 16) | (nu & 0xffff);
     const int s_lp = perm_i(dst, __float_as_int(lp));
@@ -313,7 +336,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     }
     // ---- compaction (kept element k -> its sorted lane) and the cyclic pad
     int k;
-    if constexpr (kV1 && kRep) {  // w < W <= 4: w % nkept by three wrapping subtractions
+    if constexpr (kV1 && kRep8) {  // w < W <= 4: w % nkept by three wrapping subtractions
       unsigned kk = (unsigned)w;
 #pragma unroll
       for (int r = 0; r < 3; ++r) kk = min(kk, kk - (unsigned)nkept);
@@ -326,7 +349,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       srcl = gbase | kth_set_bit<NMAX>(kmask, k);
     } else {  // (wider masks: the search costs more than the permute round trip it saves)
       const int cdst = keep ? __popcll(kmask & below) : nkept + __popcll(~kmask & below);
-      srcl = bperm_i(k, perm_i(cdst, lane));
+      srcl = bperm_i(gbase | k, perm_i(gbase | cdst, lane));
     }
     const int g_lp = bperm_i(srcl, s_lp), g_ntu = bperm_i(srcl, s_ntu), g_pk = bperm_i(srcl, s_pk);
     const int g_tot = kV2 ? bperm_i(srcl, s_tot) : 0;

@@ -234,6 +234,8 @@ print("unreachable")
     (6, 37, 20, 1),    # W = 1, T not a multiple of the 4-row prefetch ring
     (7, 33, 24, 2),    # n = 4 and n = 6: 8-lane candidate replicas with idle lanes in each
     (5, 41, 50, 3),
+    (4, 30, 40, 6),    # n = 12 (4 replicas of 16 lanes) and n = 24 (2 replicas of 32)
+    (3, 28, 60, 12),
     (5, 70, 130, 4),   # U > 128: rows read from HBM directly; T spans three 32-step flushes
     (4, 40, 30, 32),   # 2W = 64 candidates: every lane holds one
     (3, 25, 16, 40),   # W > 32: the LDS step_wave kernel
