@@ -253,29 +253,55 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     }
     // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
     const unsigned khi = lp_key(lp);
-    const u64 key = ((u64)(valid ? khi : 0u) << 32) | (unsigned)(63 - c);
+    // kSign (>= 32 compares per lane): a 63-bit key (high word shifted by 31), so a difference of
+    // two keys never overflows and its sign bit is the comparison; else (khi, 63 - c) as a pair
+    constexpr int kJN = kRep8 ? 1 : NMAX / kReps;
+    constexpr bool kSign = kJN >= 32;
+    const u64 key = ((u64)(valid ? khi : 0u) << (kSign ? 31 : 32)) | (unsigned)(63 - c);
     int rank = 0;
+    // count the keys in kr[0, JN) (stored negated) that beat this lane's: key + (-key_j) has its
+    // sign bit set iff key_j > key; the signs are shifted into a bit mask by v_alignbit and
+    // counted per 32 -- no compare into an SGPR mask, so no VALU -> SGPR -> VALU hazard waits
+    auto count_beats = [&](const u64* kr, auto jn) {
+      constexpr int JN = decltype(jn)::value;
+      int r = 0;
+      if constexpr (!kSign) {  // keys stored as they are
+#pragma unroll
+        for (int j = 0; j < JN; j += 2) {
+          const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(kr + j);  // broadcast read
+          r += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
+        }
+        return r;
+      }
+      unsigned bits = 0;
+#pragma unroll
+      for (int j = 0; j < JN; j += 2) {
+        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(kr + j);  // broadcast read
+        bits = __builtin_amdgcn_alignbit(bits, (unsigned)((key + kk.x) >> 32), 31);
+        bits = __builtin_amdgcn_alignbit(bits, (unsigned)((key + kk.y) >> 32), 31);
+        if ((j + 2) % 32 == 0 || j + 2 >= JN) {
+          r += __popc(bits);
+          bits = 0;
+        }
+      }
+      return r;
+    };
     if constexpr (kRep8) {
       // lane 8x + y compares its candidate y with candidate x (read from lane x): bit 8x + y of
       // the ballot says y sorts before x, so candidate x's rank is the popcount of byte x
       const int xl = lane >> 3;
       const unsigned klo = (unsigned)bperm_i(xl, (int)(unsigned)key);
       const unsigned khx = (unsigned)bperm_i(xl, (int)(unsigned)(key >> 32));
-      const u64 beats = ballot(key > (((u64)khx << 32) | klo));
+      const u64 beats = ballot(key > (((u64)khx << 32) | klo));  // (63-bit keys compare as u64)
       rank = __popc((unsigned)(beats >> (8 * c)) & 0xffu);
     } else if constexpr (kRep) {
       // replica r counts the keys [r JN, (r + 1) JN) of replica 0 that beat its candidate (reads
       // broadcast within the replica); the partial counts are summed across replicas by swapping
       // 16-lane rows and 32-lane halves
       constexpr int JN = NMAX / kReps;
-      keys[lane] = key;
+      keys[lane] = kSign ? 0ull - key : key;
       lds_order();
-      const u64* kr = keys + (lane / NMAX) * JN;
-#pragma unroll
-      for (int j = 0; j < JN; j += 2) {
-        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(kr + j);
-        rank += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
-      }
+      rank = count_beats(keys + (lane / NMAX) * JN, std::integral_constant<int, JN>{});
       lds_order();
       if constexpr (kReps == 4) {
         const auto r16 = __builtin_amdgcn_permlane16_swap(rank, rank, false, false);
@@ -284,14 +310,10 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       const auto r32 = __builtin_amdgcn_permlane32_swap(rank, rank, false, false);
       rank = (int)(r32[0] + r32[1]);
     } else {
-      keys[lane] = key;
+      keys[lane] = kSign ? 0ull - key : key;
       lds_order();
-      // keys of lanes >= n are below every valid key (their high word is 0): reading them is harmless
-#pragma unroll
-      for (int j = 0; j < NMAX; j += 2) {
-        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(keys + j);  // broadcast read
-        rank += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
-      }
+      // keys of lanes >= n are below every valid key (their high bits are 0): reading them is harmless
+      rank = count_beats(keys, std::integral_constant<int, NMAX>{});
       lds_order();
     }
     const u64 vmask = ballot(valid != 0) & kGrp;
