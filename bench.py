@@ -15,7 +15,8 @@ roofline: algorithmic HBM bytes of the fwd-bwd kernel = 16 B/cell (read 2xf32 lo
 with HIP events on the launch stream around the K back-to-back launches of the timed region
 (so it includes the ~1 us gaps between launches); peak 8 TB/s (MI355X_MICROARCH.md).
 traffic: HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
-null when absent.
+reported only when that summary was taken of the same kernel instance (ssnt_fwd_bwd_last_kernel),
+built from the same sources (sha256 of csrc/ + header) on the same workload; null otherwise.
 cpu_baseline: the C oracle (oracle/ssnt_oracle.c, same split-exponent arithmetic; the reference
 has no forward-backward) on this host's cores, rank 0 at N=1 only.
 
@@ -101,15 +102,36 @@ def cpu_baseline(B, T, U):
             "single_thread_value": single, "host": info}
 
 
-def pmc_traffic():
+def kernel_source_sha():
+    """sha256 over the kernel sources and the public header (what the .so is built from)."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted((ROOT / "ssnt-tts-rust_amd" / "csrc").glob("*")) + [ROOT / "include" / "ssnt_tts_c.h"]
+    for f in files:
+        if f.suffix in (".hip", ".h"):
+            h.update(f.name.encode())
+            h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel, source_sha, B, T, U):
+    """HBM bytes per launch from the committed PMC summary (tools/pmc_traffic.py), only when that
+    summary was taken of the same kernel instance, built from the same sources, on the same
+    workload as this run; else (None, why)."""
     p = ROOT / "profiles" / "pmc_fwd_bwd.json"
     if not p.exists():
-        return None
+        return None, "no PMC summary"
     try:
         d = json.loads(p.read_text())
-        return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+    except ValueError:
+        return None, "unreadable PMC summary"
+    if d.get("dispatch") != kernel:
+        return None, f"PMC summary is of {d.get('dispatch')!r}, this run dispatched {kernel!r}"
+    if d.get("source_sha") != source_sha:
+        return None, f"PMC summary taken at sources {d.get('source_sha')}, these are {source_sha}"
+    if d.get("workload") != [B, T, U]:
+        return None, f"PMC summary workload {d.get('workload')} != {[B, T, U]}"
+    return d.get("hbm_bytes_per_launch"), f"profiles/{d.get('tag')}_fwd_bwd_summary.json"
 
 
 def main():
@@ -152,6 +174,7 @@ def main():
 
     # correctness/status check once through the full Python mirror, outside the timed region
     r = S.ssnt_fwd_bwd(lt, sl, pl, out=out, check=True, loss_sum=True)
+    kernel = S.last_fwd_bwd_kernel()  # the instance the timed launches dispatch (same shapes)
     assert torch.isfinite(r["loss"]).all()
     assert torch.isclose(r["loss_sum"], r["loss"].double().sum().float(), rtol=1e-5).all()
 
@@ -208,7 +231,7 @@ def main():
         # every step's reduced sum is the global batch loss (one shard per rank)
         assert torch.isfinite(sums).all()
     if rank == 0:
-        res = result_line(world, B, T, U, K, args.warmup, elapsed, kern_ms, dist)
+        res = result_line(world, B, T, U, K, args.warmup, elapsed, kern_ms, dist, kernel)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(B, T, U)
         print(json.dumps(res), flush=True)
@@ -233,8 +256,10 @@ def timed_region(replay, sums, reduce, sync, barrier):
     return time.perf_counter() - t0
 
 
-def result_line(world, B, T, U, K, warmup, elapsed, kern_ms, dist):
+def result_line(world, B, T, U, K, warmup, elapsed, kern_ms, dist, kernel=None):
     cells_step = world * B * T * U
+    sha = kernel_source_sha()
+    traffic, traffic_src = pmc_traffic(kernel, sha, B, T, U)
     value = cells_step * K / elapsed
     achieved = B * T * U * BYTES_PER_CELL / (kern_ms * 1e-3) / 1e9  # GB/s per GPU
     return {
@@ -257,7 +282,8 @@ def result_line(world, B, T, U, K, warmup, elapsed, kern_ms, dist):
                                    "per-step loss sums" if dist else "single GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS,
-                     "traffic": pmc_traffic(),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": kernel, "source_sha": sha,
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": B * T * U * BYTES_PER_CELL},
     }
 

@@ -120,7 +120,9 @@ int ssnt_version(char *buf, size_t len);
  * grad_obs (B,T,U) = d loss / d log_obs (NULL = skip); log_alpha / log_beta (B,T,U) debug
  * outputs (NULL = skip). Cells outside (S_b,P_b) get grad 0 and log-alpha/beta -inf.
  * Device variant: all pointers are device pointers; `stream` is a hipStream_t (NULL = legacy
- * default); `workspace` must hold ssnt_fwd_bwd_workspace_size() bytes (may be 0 -> NULL);
+ * default); `workspace` must hold ssnt_fwd_bwd_workspace_size() bytes -- 0 (NULL workspace)
+ * when every row of the default dispatch stays in LDS (U <= 256 and T*U small enough), else the
+ * segmented kernel's (T+1)*U rows per utterance; query it after ssnt_fwd_bwd_set_variant;
  * `status` (device int, may be NULL) receives error bits. Asynchronous. */
 size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos);
 /* Kernel variant for the forward-backward (results are bit-identical): 0 = default dispatch
@@ -129,6 +131,11 @@ size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos);
  * Process-wide; env SSNT_FWD_BWD_KERNEL=simple selects 1 at first use. For A/B timing and
  * debugging. */
 int ssnt_fwd_bwd_set_variant(int variant);
+/* Name of the forward-backward kernel instance the calling thread's last ssnt_fwd_bwd* call
+ * dispatched (e.g. "k_fwd_bwd_stream<K=2,OBS=0,LDS=1,NC=3,NH=4,RS=0,NV=0>"; launches of one call
+ * joined by '+'), copied into buf (truncated to len); returns its full length. Lets a profile be
+ * matched to the kernel a benchmark actually ran. */
+int ssnt_fwd_bwd_last_kernel(char *buf, size_t len);
 int ssnt_fwd_bwd_device(const float *log_trans, const float *log_obs, const int *step_len,
                         const int *pos_len, int batch, int max_steps, int max_pos, int flags,
                         float *loss, float *grad_trans, float *grad_obs, float *log_alpha,
@@ -200,7 +207,10 @@ int ssnt_tone_latent_beam_search_decode_device(const float *h, const float *log_
                                                int *next_u, bool *next_is_finished,
                                                int *beam_branch, int *status, void *stream);
 
-/* Fused T-step v1 decode over a (B,T,U,2) log-prob lattice: step s feeds each beam
+/* Fused multi-step decodes (the three entries below) pack next_t / next_u into 16 bits each:
+ * max_steps > 32767 returns SSNT_ERR_UNSUPPORTED, and so does beam_width > 64 for v1 (v2 / tone
+ * take any W*C through the LDS step kernel).
+ * Fused T-step v1 decode over a (B,T,U,2) log-prob lattice: step s feeds each beam
  * h = lattice[b, u, t, :]; all beams start at t=u=0, log-prob 0. Per-step outputs (B,T,W);
  * best_beam_branch / best_t_history (B,T) = backtrace of slot 0 after the last step with
  * t_history = next_t (src/util.rs:20-33). */

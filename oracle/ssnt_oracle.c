@@ -931,7 +931,8 @@ int oracle_omp_max_threads(void) {
  *   unless test_mode:    the new total inside total_duration_bounds(t) (src/v2.rs:94-104,131),
  *                        !will_overrun(t) (src/v2.rs:106-111,133),
  *                        at t = I-1 the new total == O (src/v2.rs:135-137).
- * Totals above max_total are outside the state space (reachable in test mode only).
+ * Totals above max_total are outside the state space (reachable in test mode only); in band
+ * mode O > max_total makes the lattice empty (loss +inf, every row -inf, grads 0).
  * Z = sum_x alpha[I][x]; loss = -ln Z (Z == 0: +inf, 0 with FLAG_ZERO_INFINITY, grads 0);
  * grad[t][i] = d loss / d logits[t][i] = -(posterior of class i at step t).
  *
@@ -1010,7 +1011,9 @@ static void f4_one(const f4_ctx *c, int Imax, const float *lg, float *loss, floa
     if (g) memset(g, 0, sizeof(float) * (size_t)Imax * D);
     for (size_t k = 0; la && k < (size_t)(Imax + 1) * X; ++k) la[k] = -INFINITY;
     for (size_t k = 0; lb && k < (size_t)(Imax + 1) * X; ++k) lb[k] = -INFINITY;
-    if (I <= 0 || I > Imax || c->O < 0) { *loss = inf_loss; return; }
+    /* no lattice: bad lengths, or (band mode) a final total O beyond max_total -- the exact
+     * final-length rule (src/v2.rs:135-137) can then never hold, so Z = 0 whatever the rows */
+    if (I <= 0 || I > Imax || c->O < 0 || (!c->test_mode && c->O > X - 1)) { *loss = inf_loss; return; }
     for (int t = 0; t < I; ++t)
         for (int i = 0; i < D; ++i)
             w[(size_t)t * D + i] = xf_exp(lg[(size_t)t * D + i], c->allow_skip || i != c->zid);

@@ -488,6 +488,12 @@ void tone_latent_levenshtein_edit_distance(const int* a, const int* b, const int
 
 int ssnt_fwd_bwd_set_variant(int variant) { return set_fwd_bwd_variant(variant); }
 
+int ssnt_fwd_bwd_last_kernel(char* buf, size_t len) {
+  const char* d = last_fwd_bwd_dispatch();
+  if (buf && len) snprintf(buf, len, "%s", d);
+  return (int)strlen(d);
+}
+
 // A/B of the host staging of the per-step reference symbols (tools/bench_step_symbols.py);
 // not part of the public header. 0 = copies, 1 = zero-copy. Returns the previous mode.
 int ssnt_set_host_staging(int mode) {

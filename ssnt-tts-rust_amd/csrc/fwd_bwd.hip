@@ -18,6 +18,8 @@
 //   stream out while the recurrence is still running.
 // Arithmetic: split-exponent xf (xf_math.h); bit-exact with oracle/ssnt_oracle.c.
 #include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -287,6 +289,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 template <int K, bool OBS, bool LDS, bool VEC>
 int launch_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
   auto kern = k_fwd_bwd<K, OBS, LDS, VEC>;
+  note_fwd_bwd_dispatch("k_fwd_bwd<K=%d,OBS=%d,LDS=%d,VEC=%d>", K, (int)OBS, (int)LDS, (int)VEC);
   // dynamic LDS above 64 KiB needs the attribute; it is per device, so it is set on every such
   // launch (a host-side call, no device work) rather than cached in a process-wide flag
   if (lds > 64 * 1024)
@@ -334,9 +337,31 @@ int variant() {
   return g_variant.load(std::memory_order_relaxed);
 }
 
+thread_local char t_dispatch[160];
+
 }  // namespace
 
+void note_fwd_bwd_dispatch(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(t_dispatch, sizeof t_dispatch, fmt, ap);
+  va_end(ap);
+}
+const char* last_fwd_bwd_dispatch() { return t_dispatch; }
+
 size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
+  // 0 when the default dispatch keeps every row in LDS whatever the call brings: U <= 256, the
+  // streaming kernel's rows fit beside its rings even with log_obs (the larger ring slots) and
+  // the narrow form's padded rows, and the two-wave kernel (what takes 4-byte-aligned tensors)
+  // fits its rows too. (The segmented kernel, variant 2, always needs the workspace.)
+  if (variant() != 2 && U <= 256) {
+    const int K = U <= 64 ? 1 : U <= 128 ? 2 : 4;
+    const size_t Up = (size_t)K * ((U + K - 1) / K);
+    const size_t rows = (size_t)T * Up * sizeof(xf);
+    const bool stream_lds = stream_head_bytes(K, U, true) + rows <= kLdsBudget;
+    const bool simple_lds = (size_t)(64 * K + 2) * sizeof(xf) + (size_t)T * U * sizeof(xf) <= kLdsBudget;
+    if (stream_lds && simple_lds) return 0;
+  }
   // the segmented kernel keeps its rows (plus beta at the cut) in the workspace at every T; one
   // size serves every kernel variant (the two-wave kernel needs B*T*U xf at most)
   // (the streaming kernel's narrow form pads rows to whole lane slices: U + 3 at most)
@@ -409,6 +434,8 @@ int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t st) {
   bool summed = false;
   const int rc = launch_variant(a, st, summed);
   if (rc != SSNT_OK || !a.loss_sum || summed) return rc;
+  const size_t n = strlen(t_dispatch);
+  snprintf(t_dispatch + n, sizeof t_dispatch - n, "+k_loss_sum");
   hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(64), 0, st, a.loss, a.B, a.loss_sum);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }

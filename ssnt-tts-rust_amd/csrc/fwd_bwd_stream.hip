@@ -1006,6 +1006,8 @@ inline bool aligned_to(const void* p, uintptr_t m) { return (reinterpret_cast<ui
 template <int K, bool OBS, bool LDS, int NC, int NH, int RS, bool NV>
 int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
   auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH, RS, NV>;
+  note_fwd_bwd_dispatch("k_fwd_bwd_stream<K=%d,OBS=%d,LDS=%d,NC=%d,NH=%d,RS=%d,NV=%d>", K, (int)OBS,
+                        (int)LDS, NC, NH, RS, (int)NV);
   // dynamic LDS above 64 KiB needs the attribute; it is per device, so it is set on every such
   // launch (a host-side call, no device work) rather than cached in a process-wide flag
   if (lds > 64 * 1024)

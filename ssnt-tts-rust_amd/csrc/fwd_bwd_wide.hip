@@ -604,6 +604,7 @@ template <int K, bool OBS, bool DBG>
 int launch_wide(const FwdBwdArgs& a, hipStream_t st) {
   const int NW = (a.U + 64 * K - 1) / (64 * K);
   const dim3 grid(a.B, 2), block(64 * NW);
+  note_fwd_bwd_dispatch("k_fwd_bwd_wide<K=%d,OBS=%d,DBG=%d,NW=%d>x2", K, (int)OBS, (int)DBG, NW);
   hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 1, DBG>), grid, block, 0, st, a);
   if (hipGetLastError() != hipSuccess) return SSNT_ERR_HIP;
   hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 2, DBG>), grid, block, 0, st, a);

@@ -51,6 +51,10 @@ size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U);
 int set_fwd_bwd_wide_lanes(int k);  // A/B: positions per lane of the long-row kernel (1 or 2)
 size_t stream_head_bytes(int K, int U, bool obs, int ring = 0);  // LDS bytes besides the lattice rows
 int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only (tools/diag_fwd_bwd.py)
+// the fwd-bwd kernel instance this thread dispatched last ("k_fwd_bwd_stream<K=2,...>"; one
+// name per launch of a multi-launch kernel, joined by '+'); for bench.py's profile check
+void note_fwd_bwd_dispatch(const char* fmt, ...);
+const char* last_fwd_bwd_dispatch();
 
 // ---- F4: v2 duration-class forward-backward (v2_fwd_bwd.hip) ----
 struct V2FwdBwdArgs {

@@ -170,7 +170,10 @@ __device__ __forceinline__ bool f4_setup(const V2FwdBwdArgs& a, int b, const int
   const bool bad_len = u.I < 0 || u.I > a.Imax || u.O < 0;
   if (report && (bad_len || neg) && threadIdx.x == 0 && a.status)
     atomicOr(a.status, neg ? kStatusBadIndex : kStatusBadLength);
-  return !(bad_len || neg || u.I == 0);
+  // band mode with O > max_total: the final total can never equal O (src/v2.rs:135-137), so the
+  // lattice is empty (= oracle f4_one); its windows could also exceed the band-sized Wcap
+  const bool beyond = !u.test && u.O > u.X - 1;
+  return !(bad_len || neg || u.I == 0 || beyond);
 }
 
 // workspace: alpha rows [B][Imax+1][Wc] | beta rows [B][Imax+1][Wc] | Z [B]

@@ -36,6 +36,7 @@ SIGNATURES = {
     "ssnt_fwd_bwd_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "ssnt_fwd_bwd_sum_state_size": (c_size_t, [c_int]),
     "ssnt_fwd_bwd_set_variant": (c_int, [c_int]),
+    "ssnt_fwd_bwd_last_kernel": (c_int, [ctypes.c_char_p, c_size_t]),
     "ssnt_fwd_bwd_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
                                     c_size_t, P, P]),
     "ssnt_fwd_bwd_sum_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
@@ -92,6 +93,13 @@ def load(require_gpu: bool = False):
         if not torch.cuda.is_available():
             raise RuntimeError("libssnt_tts_c: no GPU visible (there is no CPU fallback)")
     return _lib
+
+
+def last_fwd_bwd_kernel() -> str:
+    """The fwd-bwd kernel instance this thread's last ssnt_fwd_bwd* call dispatched."""
+    buf = ctypes.create_string_buffer(256)
+    load().ssnt_fwd_bwd_last_kernel(buf, 256)
+    return buf.value.decode()
 
 
 def status_string(code: int) -> str:

@@ -22,10 +22,16 @@ def shard_bounds(global_batch: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def sharded_loss(per_utt_loss: torch.Tensor, group=None, average_over: int | None = None):
+def sharded_loss(per_utt_loss: torch.Tensor | None, group=None, average_over: int | None = None,
+                 shard_sum: torch.Tensor | None = None):
     """Sum this shard's per-utterance losses and all-reduce the scalar across ranks.
+    `shard_sum` (1,) is a shard sum already formed on device (the library's in-launch fixed-order
+    sum, ssnt_fwd_bwd_sum_device); it is used as is instead of re-summing `per_utt_loss`.
     `average_over` (the global batch) turns the sum into the global mean."""
-    total = per_utt_loss.sum(dim=0, keepdim=True).to(torch.float32)
+    if shard_sum is not None:
+        total = shard_sum.reshape(1).to(torch.float32).clone()
+    else:
+        total = per_utt_loss.sum(dim=0, keepdim=True).to(torch.float32)
     if torch.distributed.is_available() and torch.distributed.is_initialized():
         torch.distributed.all_reduce(total, op=torch.distributed.ReduceOp.SUM, group=group)
     if average_over:
@@ -53,4 +59,7 @@ def sharded_fwd_bwd(log_trans_global, step_len_global, pos_len_global, *,
     loss = res["loss"]
     if not isinstance(loss, torch.Tensor):
         loss = torch.as_tensor(loss)
-    return sharded_loss(loss), res, (lo, hi)
+    shard_sum = res.get("loss_sum")  # (fwd_bwd called with loss_sum=True: formed in the launch)
+    if shard_sum is not None and not isinstance(shard_sum, torch.Tensor):
+        shard_sum = torch.as_tensor(shard_sum)
+    return sharded_loss(loss, shard_sum=shard_sum), res, (lo, hi)

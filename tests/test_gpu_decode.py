@@ -236,7 +236,7 @@ print("unreachable")
     (5, 41, 50, 3),
     (4, 30, 40, 6),    # n = 12 (4 replicas of 16 lanes) and n = 24 (2 replicas of 32)
     (3, 28, 60, 12),
-    (5, 70, 130, 4),   # U > 128: rows read from HBM directly; T spans three 32-step flushes
+    (5, 70, 130, 4),   # U > 128: rows read from HBM directly (the whole history fits LDS)
     (4, 40, 30, 32),   # 2W = 64 candidates: every lane holds one
     (3, 25, 16, 40),   # W > 32: the LDS step_wave kernel
 ])
@@ -252,3 +252,28 @@ def test_lattice_decode_paths(gpu, oracle, shape, tie_rich):
     got = gpu.lattice_beam_search_decode(_t(lat), _t(il), W)
     for k, v in want.items():
         assert np.array_equal(got[k].cpu().numpy(), v), k
+
+
+def test_v1_seven_step_reference_sequence(gpu, oracle, golden):
+    # ssnt-tts-tensorflow/tests/test_beam_search_op.py:11-34: the reference's only multi-step v1
+    # op sequence (W=3, max_t=4), fed step by step through the exact symbol the TF op binds
+    # (ssnt_tts_beam_search_decode, host pointers, batch 1) and through the batched device entry;
+    # every step's six outputs bit-exact against the oracle, the state carried like the op loop.
+    from ssnt_tts_amd import capi
+    fx = golden["v1_seven_step_inputs"]
+    W, T = fx["beam_width"], fx["max_t"]
+    assert len(fx["acts_bits"]) == 7
+    hist = np.zeros(W, np.float32)
+    t = np.zeros(W, np.int32)
+    u = np.zeros(W, np.int32)
+    fin = np.zeros(W, bool)
+    for step, bits in enumerate(fx["acts_bits"]):
+        h = np.array(bits, np.uint32).view(np.float32).reshape(W, 2)
+        o = oracle.v1_step(h[None], hist[None], fin[None], t[None], u[None], [T])
+        want = {k: v[0] for k, v in o.items()}
+        g = capi.ssnt_tts_beam_search_decode(h, hist, fin, t, u, T, W)
+        _eq(g, want, V1_KEYS, f"host symbol step={step}")
+        gd = gpu.beam_search_decode(_t(h[None]), _t(hist[None]), _t(fin[None]), _t(t[None]),
+                                    _t(u[None]), _t(np.array([T], np.int32)), W)
+        _eq([x[0] for x in gd], want, V1_KEYS, f"device step={step}")
+        hist, t, u, fin = want["log_prob"], want["next_t"], want["next_u"], want["next_is_finished"]

@@ -225,3 +225,58 @@ def test_nan_inputs_stay_in_range(gpu, oracle, kind):
     o = oracle.tone_lattice_decode(lg, il, 0)
     g = gpu.tone_latent_lattice_beam_search_decode(_t(lg), _t(il), 4, 0)
     _same(g, o, ("beam_branch", "ordered_beam_branch", "prediction"), "nan tone")
+
+
+# Long decodes: the register kernel's two other history layouts. WHOLE (every per-step record in
+# LDS, one flush after the loop) holds while T*W <= ~4700 (RegLayout in fused_decode.hip); past
+# that the records are flushed every 32 steps with the (parent, aux[, total]) history kept in
+# LDS for the in-launch backtrace; past ~150 KB of history (nh*4*T*W bytes) the history stays in
+# the global outputs and k_fused_paths backtraces from there.
+@pytest.mark.parametrize("T,U,W,ctx", [
+    (1500, 80, 4, "chunked flush, history in LDS, staged rows"),
+    (1300, 300, 4, "chunked flush, history in LDS, rows from HBM"),
+    (700, 40, 32, "history beyond LDS: k_fused_paths"),
+])
+@pytest.mark.parametrize("tie_rich", [False, True])
+def test_v1_long_history_layouts(gpu, oracle, T, U, W, ctx, tie_rich):
+    B = 5
+    lat = (oracle.synth_tie_rich_log_trans(B, T, U, seed=T + W) if tie_rich
+           else oracle.synth_log_trans(B, T, U, seed=T + W))
+    il = np.random.default_rng(T).integers(U // 2, U + 1, size=B).astype(np.int32)
+    il[0] = U
+    want = oracle.v1_lattice_decode(lat, il, W)
+    got = gpu.lattice_beam_search_decode(_t(lat), _t(il), W)
+    for k, v in want.items():
+        g = got[k].cpu().numpy()
+        if not np.array_equal(g, v):
+            bad = np.argwhere(g != v)
+            raise AssertionError(f"{ctx} {k}: {len(bad)} mismatches, first at {bad[0].tolist()}")
+
+
+def test_v2_long_chunked_flush(gpu, oracle):
+    # I=1500 steps at W=4, D=16 (T*W = 6000): chunked flush with the 3-array history in LDS; the
+    # band and exact-length rules decide every step (O = 5 I)
+    lg, il, ol, _ = _config5(oracle, 31, B=4, I=1500, O=7500, D=16, W=4)
+    _v2(gpu, oracle, lg, np.arange(16, dtype=np.int32), il, ol, 0, False, False, "v2 I=1500")
+
+
+def test_v2_history_beyond_lds(gpu, oracle):
+    # W=16, D=4 (64 candidates, one per lane), I=1000 test-mode steps: 3*4*T*W = 192 KB of
+    # history > LDS, so the paths come from k_fused_paths over the global outputs
+    B, I, W, D = 3, 1000, 16, 4
+    lg = oracle.synth_tone_logits(B, I, W, D, seed=32)
+    il = np.array([1000, 990, 700], np.int32)
+    _v2(gpu, oracle, lg, np.arange(D, dtype=np.int32), il, np.zeros(B, np.int32), 0, True, True,
+        "v2 W=16 D=4 I=1000 test_mode")
+
+
+@pytest.mark.parametrize("T,W,C,ctx", [
+    (1500, 4, 5, "chunked flush, history in LDS"),
+    (500, 64, 1, "history beyond LDS: k_fused_paths"),
+])
+def test_tone_long_history_layouts(gpu, oracle, T, W, C, ctx):
+    B = 4
+    lg = oracle.synth_tone_logits(B, T, W, C, seed=T + C, tie_rich=True)
+    il = np.random.default_rng(T).integers(T // 2, T + 1, size=B).astype(np.int32)
+    il[0] = T
+    _tone(gpu, oracle, lg, il, 0, ctx)

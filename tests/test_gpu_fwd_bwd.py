@@ -289,6 +289,54 @@ def test_fused_loss_sum_more_workgroups_than_cus(gpu, oracle, kernel_variant):
         assert r["loss_sum"].cpu().numpy()[0] == _wave_order_sum(o["loss"])
 
 
+_C3 = {}
+
+
+def _config4_oracle(oracle):
+    """BASELINE configs[3] (B=2048 T=200 U=80, full lengths, seed 3): the oracle once per session."""
+    if not _C3:
+        B, T, U = 2048, 200, 80
+        lt = oracle.synth_log_trans(B, T, U, seed=3)
+        _C3.update(lt=lt, o=oracle.fwd_bwd_xf(lt, [T] * B, [U] * B))
+    return _C3["lt"], _C3["o"]
+
+
+def test_config4_global_batch_whole_and_sharded(gpu, oracle):
+    # BASELINE configs[3]: B=2048 T=200 U=80, the global batch the 8-GPU run shards. On one GPU:
+    # (1) the whole batch in one launch; (2) distributed.sharded_fwd_bwd over the 8 explicit
+    # (rank, world=8) shards in sequence -- the exact slices each rank of the 8-GPU job runs.
+    # Utterances are independent (src/lib.rs:122-133), so every shard is bit-exact against the
+    # oracle's rows of the global batch, and the fused in-launch shard sum equals the library's
+    # fixed-order sum of that shard.
+    from ssnt_tts_amd.distributed import sharded_fwd_bwd, shard_bounds
+    dev = torch.device("cuda:0")
+    lt, o = _config4_oracle(oracle)
+    B, T, U = lt.shape[:3]
+    x = torch.from_numpy(lt).to(dev)
+    sl = torch.full((B,), T, dtype=torch.int32, device=dev)
+    pl = torch.full((B,), U, dtype=torch.int32, device=dev)
+    r = gpu.ssnt_fwd_bwd(x, sl, pl, loss_sum=True, check=True)
+    _assert_bit_exact({k: v.cpu().numpy() for k, v in r.items() if k in ("loss", "grad")}, o,
+                      ["loss", "grad"])
+    full_sum = r["loss_sum"].cpu().numpy()[0]
+    assert full_sum == _wave_order_sum(o["loss"])
+    del r
+    shard_sums = []
+    for rank in range(8):
+        total, res, (lo, hi) = sharded_fwd_bwd(x, sl, pl, rank=rank, world=8, loss_sum=True,
+                                               check=True)
+        assert (lo, hi) == shard_bounds(B, 8, rank) and hi - lo == 256
+        _assert_bit_exact({"loss": res["loss"].cpu().numpy(), "grad": res["grad"].cpu().numpy()},
+                          {"loss": o["loss"][lo:hi], "grad": o["grad"][lo:hi]}, ["loss", "grad"])
+        assert res["loss_sum"].cpu().numpy()[0] == _wave_order_sum(o["loss"][lo:hi])
+        assert float(total) == float(res["loss_sum"].cpu().numpy()[0])  # (no process group: local)
+        shard_sums.append(float(total))
+    # the 8 ranks' all-reduce (a sum of 8 f32 shard sums) vs the one-launch global sum
+    want = float(np.sum(o["loss"], dtype=np.float64))
+    assert abs(sum(shard_sums) - want) <= 1e-5 * abs(want)
+    assert abs(float(full_sum) - want) <= 1e-5 * abs(want)
+
+
 @pytest.mark.parametrize("shape", [(2, 30, 700), (2, 24, 1024), (3, 26, 777)])
 def test_rows_beyond_512_bit_exact(gpu, oracle, kernel_variant, shape):
     # 512 < U <= 1024: only the segmented kernel (two positions per lane, 8 waves per direction)
@@ -324,5 +372,48 @@ def test_offset_and_odd_shapes(gpu, oracle, kernel_variant, shift, U):
     r = gpu.ssnt_fwd_bwd(x, torch.tensor(S, dtype=torch.int32, device=dev),
                          torch.tensor(P, dtype=torch.int32, device=dev), debug=True, check=True)
     g = {k: v.cpu().numpy() for k, v in r.items() if k != "status"}
+    o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
+    _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+
+
+LIVE_WIDE = [  # (B, T, U) with T >= U: every wave of the segmented kernel carries live positions
+    (2, 1030, 1024),  # 2 positions per lane, 8 waves per direction
+    (2, 920, 900),    # 2 per lane, 8 waves (last one partly live)
+    (2, 520, 500),    # 1 per lane, 8 waves
+    (3, 512, 480),    # 1 per lane, 8 waves (last one partly live)
+]
+
+
+@pytest.mark.parametrize("shape", LIVE_WIDE)
+def test_rows_beyond_512_live_every_wave(gpu, oracle, kernel_variant, shape):
+    # The segmented kernel's wave pipeline (5..8 waves per direction handing boundary values
+    # through LDS) with live positions in every wave: utterance 0 spans the full U x T lattice,
+    # the others are ragged with P past the first wave's 64K positions.
+    if kernel_variant == 1 and shape[2] > 512:
+        pytest.skip("the two-wave kernel stops at U = 512")
+    B, T, U = shape
+    rng = np.random.default_rng(T + U)
+    lt = oracle.synth_log_trans(B, T, U, seed=T + U)
+    P = [U] + [int(x) for x in rng.integers(U // 2, U + 1, size=B - 1)]
+    S = [T] + [int(rng.integers(p, T + 1)) for p in P[1:]]
+    g = _run_gpu(gpu, lt, S, P, debug=False)
+    o = oracle.fwd_bwd_xf(lt, S, P)
+    _assert_bit_exact(g, o, ["loss", "grad"])
+    assert np.all(np.isfinite(g["loss"]))
+
+
+@pytest.mark.parametrize("U", [500, 1000])
+def test_rows_beyond_512_live_ragged_batch(gpu, oracle, wide_lanes, kernel_variant, U):
+    # a ragged batch over the segmented kernel's range, both lane widths where U allows (one
+    # position per lane stops at U = 512), debug rows too
+    if kernel_variant == 1 and U > 512:
+        pytest.skip("the two-wave kernel stops at U = 512")
+    if wide_lanes == 1 and U > 512:
+        pytest.skip("one position per lane stops at U = 512 (the K2 case covers it)")
+    B, T = 6, U + 40
+    lt = oracle.synth_log_trans(B, T, U, seed=11)
+    P = np.array([U, U - 1, (2 * U) // 3, U // 2 + 13, 129, 1])
+    S = np.array([T, U - 1, U - 50, (3 * U) // 4, T, 3])
+    g = _run_gpu(gpu, lt, S, P)
     o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
     _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])

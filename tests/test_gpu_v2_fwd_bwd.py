@@ -125,3 +125,22 @@ def test_negative_duration_is_reported(gpu):
     logits = np.zeros((2, 3, 3), np.float32)
     with pytest.raises(gpu.SsntError):
         _run(gpu, logits, [0, -1, 2], [3, 3], [4, 4], max_total=6)
+
+
+@pytest.mark.parametrize("zero_infinity", [False, True])
+def test_band_mode_output_length_beyond_max_total(gpu, oracle, zero_infinity):
+    # band mode with O > max_total (e.g. I=100, O=1000, max_total=20): the band windows of the
+    # early rows are wider than the band-sized row capacity, and the exact final total can never
+    # be reached, so the lattice is empty: loss +inf (0 under zero_infinity), grads 0, rows -inf
+    rng = np.random.default_rng(21)
+    B, Imax, D = 3, 100, 8
+    logits = rng.standard_normal((B, Imax, D)).astype(np.float32)
+    table = np.arange(D, dtype=np.int32)
+    I = np.array([100, 100, 40], np.int32)
+    O = np.array([1000, 300, 21], np.int32)
+    g = _run(gpu, logits, table, I, O, 0, True, False, 20, zero_infinity=zero_infinity)
+    o = oracle.v2_fwd_bwd(logits, table, I, O, 20, 0, True, False,
+                          flags=oracle.FLAG_ZERO_INFINITY if zero_infinity else 0, debug=True)
+    _same(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+    assert np.all(g["loss"] == (0.0 if zero_infinity else np.inf))
+    assert not g["grad"].any()

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """GPU time of the fwd-bwd at the shapes the streaming kernel declines:
 U % K != 0, tensors at an element offset, 512 < U <= 1024 -- default dispatch vs the two-wave
-kernel. One JSON line per (shape, variant)."""
+kernel. One JSON line per (shape, variant). Every timed lattice is feasible (T >= U, full
+lengths): an infeasible one (S < P) only zero-fills grad and would time a memset, not the
+recurrence, so such shapes are rejected before anything runs."""
 import json
 import sys
 from pathlib import Path
@@ -21,6 +23,9 @@ DEV = torch.device("cuda:0")
 
 
 def case(B, T, U, shift, variant):
+    if T < U:
+        raise ValueError(f"infeasible timing shape B={B} T={T} U={U}: every utterance has S < P, "
+                         "so the kernel would only zero-fill grad")
     lib = S.load()
     if lib.ssnt_fwd_bwd_set_variant(variant) != 0:
         return None
@@ -37,13 +42,16 @@ def case(B, T, U, shift, variant):
     except Exception as e:  # noqa: BLE001 -- a kernel that declines the shape
         return {"B": B, "T": T, "U": U, "offset_floats": shift, "variant": variant, "error": str(e)[:80]}
     t = gpu_time(lambda: S.ssnt_fwd_bwd(x, sl, pl, out=out), 10)
-    return {"B": B, "T": T, "U": U, "offset_floats": shift, "variant": variant, "gpu_us": t * 1e6}
+    loss = out["loss"].cpu().numpy()
+    assert np.isfinite(loss).all(), "a timed lattice must be feasible"
+    return {"B": B, "T": T, "U": U, "offset_floats": shift, "variant": variant, "gpu_us": t * 1e6,
+            "cells_per_s": B * T * U / t}
 
 
 if __name__ == "__main__":
     for (B, T, U, shift) in [(256, 200, 80, 0), (256, 200, 81, 0), (256, 200, 127, 0), (256, 200, 80, 1),
-                             (256, 200, 80, 2), (256, 200, 120, 0), (64, 400, 700, 0),
-                             (64, 400, 1024, 0)]:
+                             (256, 200, 80, 2), (256, 200, 120, 0), (64, 400, 300, 0),
+                             (64, 760, 700, 0), (64, 1100, 1024, 0)]:
         for v in (0, 1):
             r = case(B, T, U, shift, v)
             if r:

@@ -5,7 +5,9 @@ Inputs (from tools/profile_gpu.sh): <dir>/kt (kernel trace + stats), <dir>/fetch
 pass), <dir>/write (WRITE_SIZE pass). Writes:
   profiles/<tag>_kernel_stats.csv     -- the rocprofv3 --stats summary (copied)
   profiles/<tag>_fwd_bwd_summary.json -- avg duration + HBM traffic per launch
-  profiles/pmc_fwd_bwd.json           -- what bench.py reports as roofline.traffic
+  profiles/pmc_fwd_bwd.json           -- what bench.py reports as roofline.traffic (with the
+                                         kernel instance, source hash and workload it was taken
+                                         on: bench.py reports it only for the same three)
 
 HBM bytes per launch, following MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE counts exactly half the bytes of a wide coalesced streaming read, so
@@ -57,6 +59,17 @@ def main():
     fetch, _ = _pmc(os.path.join(d, "fetch"), "FETCH_SIZE")
     write, _ = _pmc(os.path.join(d, "write"), "WRITE_SIZE")
     summ = {"tag": tag, "kernel": KERNEL_KEY, "launches": len(durs)}
+    names = sorted({r.get("Kernel_Name") for r in trace if KERNEL_KEY in (r.get("Kernel_Name") or "")})
+    summ["kernel_names"] = names
+    # the bench line printed under the profiler names the dispatched instance and the sources
+    for logf in glob.glob(os.path.join(d, "kt*.log")) + glob.glob(os.path.join(d, "kt", "*.log")):
+        for line in Path(logf).read_text(errors="replace").splitlines():
+            if line.startswith("{") and '"roofline"' in line:
+                rl = json.loads(line)["roofline"]
+                cfg = json.loads(line)["config"]
+                summ["dispatch"] = rl.get("kernel")
+                summ["source_sha"] = rl.get("source_sha")
+                summ["workload"] = [cfg["global_batch"] // json.loads(line)["n_gpus"], cfg["T"], cfg["U"]]
     if durs:
         summ["avg_us"] = statistics.mean(durs)
         summ["median_us"] = statistics.median(durs)
@@ -71,7 +84,7 @@ def main():
             "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; KiB->B",
         })
     (prof / f"{tag}_fwd_bwd_summary.json").write_text(json.dumps(summ, indent=1))
-    if "hbm_bytes_per_launch" in summ:
+    if "hbm_bytes_per_launch" in summ and "dispatch" in summ:
         (prof / "pmc_fwd_bwd.json").write_text(json.dumps(summ, indent=1))
     print(json.dumps(summ, indent=1))
 
