@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <vector>
 
 #include "ssnt_internal.h"
@@ -118,6 +119,27 @@ int ensure(size_t dbytes, size_t hbytes, const char* fn, bool abort_on_error) {
   return SSNT_OK;
 }
 
+// Per-phase host clock of the per-step reference symbols (tools/bench_step_symbols.py
+// --breakdown; diagnostics, off unless enabled): 0 entry -> context ready, 1 -> inputs staged,
+// 2 -> kernel launched, 3 -> synchronised (outputs visible), 4 -> outputs scattered.
+struct PhaseClock {
+  bool on = false;
+  int calls = 0;
+  double acc[5] = {0, 0, 0, 0, 0};
+  std::chrono::steady_clock::time_point last;
+  void start() {
+    if (on) last = std::chrono::steady_clock::now();
+  }
+  void mark(int k) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    acc[k] += std::chrono::duration<double, std::micro>(now - last).count();
+    last = now;
+    if (k == 4) ++calls;
+  }
+};
+thread_local PhaseClock g_clk;
+
 // Host staging mode for the small per-step reference symbols (not ssnt_fwd_bwd, whose tensors
 // are large): 0 = one H2D copy of inputs + zeroed status word, kernel, one D2H copy; 1 =
 // zero-copy: the kernel reads its inputs from and writes its outputs to the pinned staging
@@ -192,8 +214,12 @@ int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device =
       memcpy(g_ctx.h + s.off, s.src, s.bytes);
       up_end = s.off + s.bytes;
     }
-  if (p.zero_copy) return SSNT_OK;
+  if (p.zero_copy) {
+    g_clk.mark(1);
+    return SSNT_OK;
+  }
   const hipError_t e = hipMemcpyAsync(g_ctx.d, g_ctx.h, up_end, hipMemcpyHostToDevice, g_ctx.stream);
+  g_clk.mark(1);
   if (e != hipSuccess) {
     if (abort_on_error) fail(fn, hipGetErrorString(e));
     return SSNT_ERR_HIP;
@@ -204,6 +230,7 @@ int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device =
 // Download status + outputs (one D2H copy, none in zero-copy mode), synchronise, scatter to the
 // caller's arrays. Returns status code.
 int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
+  g_clk.mark(2);
   if (launch_rc != SSNT_OK) {
     if (abort_on_error) fail(fn, ssnt_status_string(launch_rc));
     return launch_rc;
@@ -218,6 +245,7 @@ int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
     if (abort_on_error) fail(fn, hipGetErrorString(e));
     return SSNT_ERR_HIP;
   }
+  g_clk.mark(3);
   int bits = 0;
   memcpy(&bits, g_ctx.h + p.status_off, sizeof(int));
   const int rc = status_bits_to_code(bits);
@@ -233,8 +261,11 @@ int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
     return rc;
   }
   for (auto& s : p.out) memcpy(s.dst, g_ctx.h + s.off, s.bytes);
+  g_clk.mark(4);
   return SSNT_OK;
 }
+
+__global__ void k_null() {}
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -281,7 +312,9 @@ void ssnt_tts_beam_search_decode(const float* h, const float* log_prob_history,
   check_ptr(next_t, fn, "next_t"); check_ptr(next_u, fn, "next_u");
   check_ptr(next_is_finished, fn, "next_is_finished"); check_ptr(beam_branch, fn, "beam_branch");
   if (beam_width <= 0) fail(fn, "chunk size must be non-zero (beam_width <= 0)");
+  g_clk.start();
   ctx_ready(fn, true);
+  g_clk.mark(0);
   const size_t W = beam_width;
   Plan p;
   const int ih = p.add_in(h, W * 2 * 4), ihist = p.add_in(log_prob_history, W * 4),
@@ -501,11 +534,48 @@ int ssnt_set_host_staging(int mode) {
   return g_host_mode.exchange(mode);
 }
 
+// A/B of the fused decodes' step ordering (tools, tests): -1 default, 0 full rank, 1 selection;
+// not part of the public header.
+int ssnt_fused_decode_select(int mode) { return set_fused_decode_select(mode); }
+
 // A/B of the long-row kernel's lane width (tools, tests); not part of the public header.
 int ssnt_fwd_bwd_wide_lanes(int k) { return set_fwd_bwd_wide_lanes(k); }
 
+// Per-step symbol latency breakdown (tools/bench_step_symbols.py); not part of the public header.
+// enable = 1 resets and starts the calling thread's phase clock; 0 stops it and writes the mean
+// microseconds of its 5 phases (PhaseClock) to out[0..4]; returns the number of calls timed.
+int ssnt_diag_step_clock(int enable, double* out) {
+  if (enable) {
+    g_clk = PhaseClock{};
+    g_clk.on = true;
+    return 0;
+  }
+  g_clk.on = false;
+  for (int k = 0; k < 5; ++k) out[k] = g_clk.calls ? g_clk.acc[k] / g_clk.calls : 0.0;
+  return g_clk.calls;
+}
+// The floor under a per-step call: an empty kernel launched on the calling thread's stream, then
+// hipStreamSynchronize, `reps` times: out[0] mean launch us, out[1] mean synchronise us.
+int ssnt_diag_null_launch(int reps, double* out) {
+  if (ctx_ready("ssnt_diag_null_launch", false) != SSNT_OK) return -1;
+  double l = 0, sy = 0;
+  for (int i = 0; i < reps; ++i) {
+    const auto t0 = std::chrono::steady_clock::now();
+    hipLaunchKernelGGL(k_null, dim3(1), dim3(64), 0, g_ctx.stream);
+    const auto t1 = std::chrono::steady_clock::now();
+    (void)hipStreamSynchronize(g_ctx.stream);
+    const auto t2 = std::chrono::steady_clock::now();
+    l += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    sy += std::chrono::duration<double, std::micro>(t2 - t1).count();
+  }
+  out[0] = reps ? l / reps : 0;
+  out[1] = reps ? sy / reps : 0;
+  return reps;
+}
+
 // diagnostic builds (make lib-diag) only; not part of the public header
 int ssnt_diag_read(void* host, size_t bytes) { return diag_read(host, bytes); }
+int ssnt_diag_decode_read(void* host, size_t bytes) { return diag_decode_read(host, bytes); }
 
 
 size_t ssnt_fwd_bwd_sum_state_size(int batch) { return batch > 0 ? fwd_bwd_sum_state_bytes(batch) : 0; }

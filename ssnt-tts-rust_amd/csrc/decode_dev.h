@@ -210,5 +210,27 @@ __device__ __forceinline__ int wave_shr1(int v) {  // lane l gets lane l-1's v (
   return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
 }
 
+// max of x over each aligned group of N lanes (N = 8, 16, 32, 64), every lane of the group ends
+// with it: quad xor moves, the half-mirror / mirror (xor 4 / 8 once the smaller groups agree) by
+// DPP, then 16- and 32-lane swaps by v_permlane16/32_swap -- VALU only, no LDS
+template <int N>
+__device__ __forceinline__ unsigned group_max_u32(unsigned x) {
+  static_assert(N == 8 || N == 16 || N == 32 || N == 64, "group size");
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false));   // xor 1
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false));   // xor 2
+  x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, false));  // 8-group
+  if constexpr (N >= 16) x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xf, 0xf, false));
+  if constexpr (N >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    x = max((unsigned)r[0], (unsigned)r[1]);
+  }
+  if constexpr (N >= 64) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    x = max((unsigned)r[0], (unsigned)r[1]);
+  }
+  return x;
+}
+__device__ __forceinline__ int readlane_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+
 }  // namespace dec
 }  // namespace ssnt

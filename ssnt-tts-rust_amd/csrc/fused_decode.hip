@@ -23,6 +23,7 @@
 // beam has u == s, so its row is lattice[b,s]); rows are prefetched kAhead steps ahead.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <type_traits>
 
 #include "buffer_ops.h"
@@ -34,6 +35,24 @@ namespace {
 using namespace dec;
 
 constexpr int kAhead = 4;    // input rows in flight
+
+// Diagnostic build only (-DSSNT_DIAG, `make lib-diag`): s_memtime cycle totals of the register
+// kernel's step phases for utterance 0 (tools/diag_decode.py): 0 candidate generation, 1 rank /
+// selection, 2 sort permute + dedup + keep ballot, 3 compaction + slot gather, 4 output staging
+// and flush, 5 between steps (row refill, loop); [6] steps. Never present in the product build.
+#ifdef SSNT_DIAG
+__device__ unsigned long long g_dec_diag[8];
+#define DSTAMP(k)                                                   \
+  do {                                                              \
+    const unsigned long long dnow_ = __builtin_amdgcn_s_memtime();  \
+    dacc[k] += dnow_ - dlast;                                       \
+    dlast = dnow_;                                                  \
+  } while (0)
+#else
+#define DSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
 
 // buffer resource over [base, base + bytes): loads past the end return 0
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* base, unsigned bytes) {
@@ -93,8 +112,15 @@ struct RegLayout {
 
 // NMAX: a compile-time bound on n (8, 16, 32 or 64): the rank loop is unrolled to NMAX so its
 // broadcast key reads are issued back to back instead of one LDS round trip per pair.
-template <Variant V, bool STAGED, int NMAX, bool WHOLE>
-__global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
+// SEL: the step's ordering by selection instead of a full rank (select_step below); the two
+// forms give identical outputs.
+// One wave per workgroup and (staged rows, history) LDS enough that one workgroup fills a CU: the
+// compiler is told one wave per SIMD, so it may spend registers on keeping loads in flight (its
+// default occupancy target of 8 waves caps a wave at 64 VGPRs, which serialised the rank's
+// broadcast key reads into one LDS round trip per two keys).
+template <Variant V, bool STAGED, int NMAX, bool WHOLE, bool SEL>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kV1 = V == Variant::V1, kV2 = V == Variant::V2;
   const int b = blockIdx.x;
@@ -189,7 +215,12 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
   };
 
   // one step; false when v2 finds no candidate (src/v2.rs:292)
+#ifdef SSNT_DIAG
+  unsigned long long dacc[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long dlast = __builtin_amdgcn_s_memtime();
+#endif
   auto step = [&](int s, float* row, const float* nrow) -> bool {
+    DSTAMP(5);
     float* nbuf = rowbuf + ((s + 1) & 1) * 64 * R;  // row s+1 (buffer last read by step s-1)
     if constexpr (kV1 && STAGED) {
 #pragma unroll
@@ -251,6 +282,88 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       nv0 = v.x;
       nv1 = v.y;
     }
+    int g_lp, g_ntu, g_pk, g_tot;
+    DSTAMP(0);
+    if constexpr (SEL) {
+      // ---- selection (src/lib.rs:161-168, src/v2.rs:280-308): only the first W kept candidates
+      // of the sorted, deduplicated list (and the v2 diagonal one) are ever used, so they are
+      // extracted one by one instead of ranking all n. A round takes the largest key among the
+      // candidates not yet extracted (group max, ties to the lowest generation index: the stable
+      // descending order), reads its fields into scalars and keeps it unless it equals the
+      // previous extracted candidate (consecutive dedup: equal to the previous extracted is equal
+      // to the last kept, eq_ignore_parent being an equivalence). Kept record k goes to lane k.
+      const unsigned key = valid ? lp_key(lp) : 0u;  // valid keys are >= 1
+      const int lpb = __float_as_int(lp);
+      const int pk = code | (fin << 7) | (w << 8);
+      const int ntu = (nt << 16) | (nu & 0xffff);
+      const int v0b = __float_as_int(nv0), v1b = __float_as_int(nv1);
+      u64 rem = ballot(valid != 0) & kGrp;  // (replicas mirror replica 0)
+      int nk = 0;
+      int r_lp = 0, r_ntu = 0, r_pk = 0, r_tot = 0, r_v0 = 0, r_v1 = 0;
+      int q_lp = 0, q_ntu = 0, q_pk = 0, q_tot = 0;
+      bool have_q = false;
+      while (rem != 0 && nk < W) {
+        const bool in = ((rem >> c) & 1ull) != 0;
+        const unsigned m = group_max_u32<NMAX>(in ? key : 0u);
+        const int sel = (int)__builtin_ctzll(ballot(in && key == m) & kGrp);
+        rem &= ~(1ull << sel);
+        const int f_lp = readlane_i(lpb, sel), f_ntu = readlane_i(ntu, sel), f_pk = readlane_i(pk, sel);
+        const int f_tot = kV2 ? readlane_i(tot, sel) : 0;
+        const bool dup = have_q && ((f_pk ^ q_pk) & 0xff) == 0 &&
+                         __int_as_float(f_lp) == __int_as_float(q_lp) && f_ntu == q_ntu && f_tot == q_tot;
+        if (!dup) {
+          const bool mine = lane == nk;
+          r_lp = mine ? f_lp : r_lp;
+          r_ntu = mine ? f_ntu : r_ntu;
+          r_pk = mine ? f_pk : r_pk;
+          if constexpr (kV2) r_tot = mine ? f_tot : r_tot;
+          if constexpr (kV1 && STAGED) {
+            r_v0 = mine ? readlane_i(v0b, sel) : r_v0;
+            r_v1 = mine ? readlane_i(v1b, sel) : r_v1;
+          }
+          ++nk;
+        }
+        q_lp = f_lp; q_ntu = f_ntu; q_pk = f_pk; q_tot = f_tot;
+        have_q = true;
+      }
+      if constexpr (kV2) {  // assert_ne!(n_results, 0) (src/v2.rs:292); v1/tone always keep one
+        if (nk == 0) return false;
+      }
+      // v2 diagonal candidate (src/v2.rs:283-289): the first kept one on the diagonal is the
+      // largest-key valid one on it -- a dedup-dropped candidate equals its kept predecessor in
+      // total and next_t, so that predecessor is on the diagonal too and comes first
+      bool have_d = false;
+      int d_lp = 0, d_ntu = 0, d_pk = 0, d_tot = 0;
+      if constexpr (kV2) {
+        if (!a.test_mode) {
+          const float diff = (float)tot - o_over_i * (float)(u64)(unsigned)nt;
+          const bool on = valid && diff >= -20.0f && diff <= 0.0f;
+          const u64 dm = ballot(on) & kGrp;
+          if (dm) {
+            const unsigned m = group_max_u32<NMAX>(on ? key : 0u);
+            const int ds = (int)__builtin_ctzll(ballot(on && key == m) & kGrp);
+            d_lp = readlane_i(lpb, ds); d_ntu = readlane_i(ntu, ds); d_pk = readlane_i(pk, ds);
+            d_tot = readlane_i(tot, ds);
+            have_d = true;
+          }
+        }
+      }
+      // slot w: kept[w % nk] (cyclic pad, src/v2.rs:293-297 / src/lib.rs:163-167), the last slot
+      // the diagonal candidate when there is one (src/v2.rs:298-308)
+      int j = w;
+      while (j >= nk) j -= nk;
+      g_lp = bperm_i(j, r_lp);
+      g_ntu = bperm_i(j, r_ntu);
+      g_pk = bperm_i(j, r_pk);
+      g_tot = kV2 ? bperm_i(j, r_tot) : 0;
+      if constexpr (kV1 && STAGED) {
+        cv0 = __int_as_float(bperm_i(j, r_v0));
+        cv1 = __int_as_float(bperm_i(j, r_v1));
+      }
+      if (have_d && w == W - 1) {
+        g_lp = d_lp; g_ntu = d_ntu; g_pk = d_pk; g_tot = d_tot;
+      }
+    } else {
     // ---- stable descending rank (src/lib.rs:161): keys are unique, so ranks are a permutation
     const unsigned khi = lp_key(lp);
     // kSign (>= 32 compares per lane): a 63-bit key (high word shifted by 31), so a difference of
@@ -266,22 +379,31 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       constexpr int JN = decltype(jn)::value;
       int r = 0;
       if constexpr (!kSign) {  // keys stored as they are
+        ulonglong2 kk[JN / 2];  // (JN <= 16: every broadcast read issued before the compares)
 #pragma unroll
-        for (int j = 0; j < JN; j += 2) {
-          const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(kr + j);  // broadcast read
-          r += (kk.x > key ? 1 : 0) + (kk.y > key ? 1 : 0);
-        }
+        for (int q = 0; q < JN / 2; ++q) kk[q] = reinterpret_cast<const ulonglong2*>(kr)[q];
+#pragma unroll
+        for (int q = 0; q < JN / 2; ++q) r += (kk[q].x > key ? 1 : 0) + (kk[q].y > key ? 1 : 0);
         return r;
       }
       unsigned bits = 0;
+      // groups of 16 keys: 8 broadcast reads issued back to back, then their compares (one LDS
+      // round trip per group instead of one per read)
+      constexpr int G = JN < 16 ? JN : 16;
 #pragma unroll
-      for (int j = 0; j < JN; j += 2) {
-        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(kr + j);  // broadcast read
-        bits = __builtin_amdgcn_alignbit(bits, (unsigned)((key + kk.x) >> 32), 31);
-        bits = __builtin_amdgcn_alignbit(bits, (unsigned)((key + kk.y) >> 32), 31);
-        if ((j + 2) % 32 == 0 || j + 2 >= JN) {
-          r += __popc(bits);
-          bits = 0;
+      for (int j0 = 0; j0 < JN; j0 += G) {
+        ulonglong2 kk[G / 2];
+#pragma unroll
+        for (int q = 0; q < G / 2; ++q) kk[q] = reinterpret_cast<const ulonglong2*>(kr + j0)[q];
+#pragma unroll
+        for (int q = 0; q < G / 2; ++q) {
+          const int j = j0 + 2 * q;
+          bits = __builtin_amdgcn_alignbit(bits, (unsigned)((key + kk[q].x) >> 32), 31);
+          bits = __builtin_amdgcn_alignbit(bits, (unsigned)((key + kk[q].y) >> 32), 31);
+          if ((j + 2) % 32 == 0 || j + 2 >= JN) {
+            r += __popc(bits);
+            bits = 0;
+          }
         }
       }
       return r;
@@ -316,6 +438,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       rank = count_beats(keys, std::integral_constant<int, NMAX>{});
       lds_order();
     }
+    DSTAMP(1);
     const u64 vmask = ballot(valid != 0) & kGrp;
     const int nvalid = __popcll(vmask);
     const u64 below = (1ull << c) - 1ull;  // candidates of this replica before this lane
@@ -366,6 +489,7 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     } else {
       k = (dk >= 0 && w == W - 1) ? dk : (w < nkept ? w : w % nkept);
     }
+    DSTAMP(2);
     int srcl;  // sorted lane of kept element k
     if constexpr (NMAX <= 16) {
       srcl = gbase | kth_set_bit<NMAX>(kmask, k);
@@ -373,17 +497,19 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
       const int cdst = keep ? __popcll(kmask & below) : nkept + __popcll(~kmask & below);
       srcl = bperm_i(gbase | k, perm_i(gbase | cdst, lane));
     }
-    const int g_lp = bperm_i(srcl, s_lp), g_ntu = bperm_i(srcl, s_ntu), g_pk = bperm_i(srcl, s_pk);
-    const int g_tot = kV2 ? bperm_i(srcl, s_tot) : 0;
+    g_lp = bperm_i(srcl, s_lp); g_ntu = bperm_i(srcl, s_ntu); g_pk = bperm_i(srcl, s_pk);
+    g_tot = kV2 ? bperm_i(srcl, s_tot) : 0;
     if constexpr (kV1 && STAGED) {
       cv0 = __int_as_float(bperm_i(srcl, s_v0));
       cv1 = __int_as_float(bperm_i(srcl, s_v1));
+    }
     }
     hist = __int_as_float(g_lp);
     bt = (int)((unsigned)g_ntu >> 16);
     bu = g_ntu & 0xffff;
     bfin = (g_pk >> 7) & 1;
     btot = g_tot;
+    DSTAMP(3);
     // ---- outputs of slot w (src/lib.rs:138-145), staged
     const int cs = WHOLE ? s : s % kChunk;
     if (writer) {
@@ -404,6 +530,10 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     if constexpr (!WHOLE) {
       if (cs == kChunk - 1 || s == T - 1) flush(s - cs, cs + 1);
     }
+    DSTAMP(4);
+#ifdef SSNT_DIAG
+    ++dacc[6];
+#endif
     return true;
   };
 
@@ -425,6 +555,10 @@ __global__ __launch_bounds__(64) void k_fused_reg(FusedDecodeArgs a, int hist_ld
     return;
   }
   if constexpr (WHOLE) flush(0, T);
+#ifdef SSNT_DIAG
+  if (b == 0 && lane == 0)
+    for (int k = 0; k < 7; ++k) g_dec_diag[k] = dacc[k];
+#endif
   if (!hist_lds) return;  // the host runs k_fused_paths over the global outputs
   // ---- backtrace of final slot `lane` (v2_util.rs:6-36 with final_branch = [0..W); util.rs:20-33
   // for slot 0 with t history = next_t)
@@ -585,6 +719,16 @@ inline int last_error() { return hipGetLastError() == hipSuccess ? SSNT_OK : SSN
 
 constexpr size_t kMaxLds = 150 * 1024;
 
+// ordering of the register kernel's step: -1 the default per variant, 0 full rank, 1 selection
+// (A/B hook ssnt_fused_decode_select; both give identical outputs)
+std::atomic<int> g_select{-1};
+bool use_select(Variant v) {
+  const int m = g_select.load(std::memory_order_relaxed);
+  if (m >= 0) return m == 1;
+  (void)v;
+  return false;  // measured slower at every BASELINE shape
+}
+
 template <typename K>
 int launch_with_lds(K kernel, size_t lds, int B, hipStream_t st, const FusedDecodeArgs& a,
                     int extra) {
@@ -609,14 +753,19 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
     const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged, whole).total;
     if (lds > kMaxLds) return SSNT_ERR_UNSUPPORTED;
     const int h = hist_lds ? 1 : 0;
+    const bool sel = use_select(V);
     auto go = [&](auto kw, auto kc) {  // (NMAX, WHOLE) instance
       constexpr int NM = decltype(kw)::value;
       constexpr bool WH = decltype(kc)::value;
       if (!staged) {  // only v1 rows can be too long to stage
-        if constexpr (V == Variant::V1) return launch_with_lds(k_fused_reg<V, false, 64, WH>, lds, a.B, st, a, h);
+        if constexpr (V == Variant::V1) {
+          return sel ? launch_with_lds(k_fused_reg<V, false, 64, WH, true>, lds, a.B, st, a, h)
+                     : launch_with_lds(k_fused_reg<V, false, 64, WH, false>, lds, a.B, st, a, h);
+        }
         return (int)SSNT_ERR_UNSUPPORTED;
       }
-      return launch_with_lds(k_fused_reg<V, true, NM, WH>, lds, a.B, st, a, h);
+      return sel ? launch_with_lds(k_fused_reg<V, true, NM, WH, true>, lds, a.B, st, a, h)
+                 : launch_with_lds(k_fused_reg<V, true, NM, WH, false>, lds, a.B, st, a, h);
     };
     auto pick = [&](auto kc) {
       if (n <= 8) return go(std::integral_constant<int, 8>{}, kc);
@@ -643,6 +792,24 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
 }
 
 }  // namespace
+
+int diag_decode_read(void* host, size_t bytes) {
+#ifdef SSNT_DIAG
+  if (bytes > sizeof(g_dec_diag)) bytes = sizeof(g_dec_diag);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dec_diag), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? (int)bytes : -1;
+#else
+  (void)host;
+  (void)bytes;
+  return -1;
+#endif
+}
+
+int set_fused_decode_select(int mode) {
+  if (mode < -1 || mode > 1) return SSNT_ERR_INVALID_ARG;
+  g_select.store(mode);
+  return SSNT_OK;
+}
 
 int launch_fused_decode(const FusedDecodeArgs& a, hipStream_t st) {
   if (a.B < 0 || a.W <= 0 || a.T <= 0 || !a.src || !a.input_length || !a.prediction ||

@@ -817,6 +817,13 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   for (int j = 0; j < kR2; ++j)
     optr[j] = act ? outr + (size_t)(d * kR2 + j) * Up + p0 : reinterpret_cast<xf*>(junk_lane);
   auto rd = [&](int j, XRow<K>& E, XRow<K>& Xx, XRow<K>& O) {
+    if (EXP(10)) {  // experiment (timing only, wrong results): the chain reads no factors
+#pragma unroll
+      for (int q = 0; q < K; ++q) {
+        E.m[q] = 0.7f; E.e[q] = 0; Xx.m[q] = 0.6f; Xx.e[q] = -1; O.m[q] = 1.0f; O.e[q] = 0;
+      }
+      return;
+    }
     float v[4 * K];
 #pragma unroll
     for (int q = 0; q < K; ++q) ld_vec<4>(v + 4 * q, reinterpret_cast<const float*>(sptr[j] + (size_t)q * nl16));
@@ -888,7 +895,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     auto hwait = [&](int r0, int r1, bool phase2) {
       (void)r0;
       wait_row(min(r1 - 1 + PF, last));
-      if (phase2) {
+      if (phase2 && !EXP(11)) {  // (experiment 11: no release polls past the cut, timing only)
         const int q = r1 - kR2;  // newest previous occupant the half-block overwrites
         if (q > M && help_seen <= q)
           help_seen = spin_until<false>([&] { return first_missing<kNH>(ctl->help[0], M); }, q + 1, a.status, dg);
@@ -958,7 +965,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     auto hwait = [&](int r0, int r1, bool ring) {
       (void)r0;
       wait_row(min(r1 - 1 + PF, last));
-      if (ring) {
+      if (ring && !EXP(11)) {
         // previous occupants: stream rows up to r1-1-kR2, read by gradient rows q and q+1
         const int q = r1 - 1 - kR2;
         if (q > c && help_seen <= q + 1)

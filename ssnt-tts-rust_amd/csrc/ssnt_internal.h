@@ -141,6 +141,8 @@ struct FusedDecodeArgs {
   int* status;
 };
 int launch_fused_decode(const FusedDecodeArgs& a, hipStream_t stream);
+int set_fused_decode_select(int mode);  // A/B: -1 default, 0 full rank, 1 selection
+int diag_decode_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only
 
 int launch_extract_best(int B, int W, int U, const int* best_final_branch, const int* beam_branch,
                         const int* t_history, int* best_beam_branch, int* best_t_history,

@@ -26,6 +26,17 @@ def _eq(gpu_out, ref, keys, ctx=""):
         assert np.array_equal(g, ref[k]), f"{ctx} {k}: gpu={g} ref={ref[k]}"
 
 
+@pytest.fixture(params=[0, 1], ids=["rank", "select"])
+def select_mode(request, gpu):
+    """The fused decodes' two step orderings (full rank / selection) must give identical outputs."""
+    import ctypes
+    lib = gpu.load()
+    lib.ssnt_fused_decode_select.restype = ctypes.c_int
+    assert lib.ssnt_fused_decode_select(request.param) == 0
+    yield request.param
+    lib.ssnt_fused_decode_select(-1)
+
+
 V1_KEYS = ("prediction", "log_prob", "next_t", "next_u", "next_is_finished", "beam_branch")
 V2_KEYS = ("prediction", "log_prob", "next_t", "next_u", "next_is_finished",
            "next_total_duration", "beam_branch")
@@ -200,7 +211,7 @@ def test_edit_distance(gpu, oracle, golden):
 
 
 @pytest.mark.parametrize("tie_rich", [False, True])
-def test_lattice_decode_config3(gpu, oracle, tie_rich):
+def test_lattice_decode_config3(gpu, oracle, tie_rich, select_mode):
     # BASELINE configs[2]: B=256, T=200 decode steps, beam 4, alignment indices bit-exact
     B, T, U, W = 256, 200, 80, 4
     lat = (oracle.synth_tie_rich_log_trans(B, T, U, seed=3) if tie_rich
@@ -241,7 +252,7 @@ print("unreachable")
     (3, 25, 16, 40),   # W > 32: the LDS step_wave kernel
 ])
 @pytest.mark.parametrize("tie_rich", [False, True])
-def test_lattice_decode_paths(gpu, oracle, shape, tie_rich):
+def test_lattice_decode_paths(gpu, oracle, shape, tie_rich, select_mode):
     # every fused-decode path (register step staged / direct, LDS step) bit-exact vs the oracle
     B, T, U, W = shape
     lat = (oracle.synth_tie_rich_log_trans(B, T, U, seed=T) if tie_rich

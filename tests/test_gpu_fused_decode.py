@@ -22,6 +22,17 @@ def _t(x):
     return torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["rank", "select"])
+def select_mode(request, gpu):
+    """The fused decodes' two step orderings (full rank / selection) must give identical outputs."""
+    import ctypes
+    lib = gpu.load()
+    lib.ssnt_fused_decode_select.restype = ctypes.c_int
+    assert lib.ssnt_fused_decode_select(request.param) == 0
+    yield request.param
+    lib.ssnt_fused_decode_select(-1)
+
+
 def _same(g, o, keys, ctx):
     for k in keys:
         gv = g[k].cpu().numpy()

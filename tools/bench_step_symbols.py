@@ -36,6 +36,48 @@ def per_call(fn, n=2000, rounds=5):
     return float(np.median(meds)) * 1e6
 
 
+def raw_v1(lib, c, n=5000):
+    """The v1 W=4 step called through ctypes with its pointers built once (no numpy wrapper in
+    the loop), GPU symbol and C oracle alike; plus the GPU call split into its host phases
+    (ssnt_diag_step_clock) and the floor under it: an empty kernel launched on the same per-thread
+    stream and synchronised (ssnt_diag_null_launch)."""
+    W = 4
+    vp = ctypes.c_void_p
+    h = np.ascontiguousarray(c["h"][0], np.float32)
+    hist = np.ascontiguousarray(c["hist"][0], np.float32)
+    fin = np.ascontiguousarray(c["fin"][0], np.bool_)
+    t = np.ascontiguousarray(c["t"][0], np.int32)
+    u = np.ascontiguousarray(c["u"][0], np.int32)
+    outs = [np.empty(W, dt) for dt in (np.int32, np.float32, np.int32, np.int32, np.bool_, np.int32)]
+    ptr = lambda a: vp(a.ctypes.data)  # noqa: E731
+    gargs = [ptr(h), ptr(hist), ptr(fin), ptr(t), ptr(u), 80, W] + [ptr(o) for o in outs]
+    f = lib.ssnt_tts_beam_search_decode
+    ol = O.lib()
+    il = np.array([80], np.int32)
+    oouts = [np.empty(W, dt) for dt in (np.int32, np.float32, np.int32, np.int32, np.bool_, np.int32)]
+    ol.oracle_v1_step.argtypes = [ctypes.c_int] * 3 + [vp] * 12
+    oargs = [1, W, W, ptr(h), ptr(hist), ptr(fin), ptr(t), ptr(u), ptr(il)] + [ptr(o) for o in oouts]
+    g = ol.oracle_v1_step
+    out = {"raw_gpu_v1_W4_us": per_call(lambda: f(*gargs), n=n),
+           "raw_cpu_v1_W4_us": per_call(lambda: g(*oargs), n=n)}
+    lib.ssnt_diag_step_clock.restype = ctypes.c_int
+    lib.ssnt_diag_step_clock.argtypes = [ctypes.c_int, vp]
+    lib.ssnt_diag_null_launch.restype = ctypes.c_int
+    lib.ssnt_diag_null_launch.argtypes = [ctypes.c_int, vp]
+    ph = np.zeros(5)
+    lib.ssnt_diag_step_clock(1, None)
+    for _ in range(n):
+        f(*gargs)
+    calls = lib.ssnt_diag_step_clock(0, ph.ctypes.data)
+    out["gpu_v1_phase_us"] = {k: float(v) for k, v in zip(
+        ("context", "stage_in", "launch", "synchronise", "scatter"), ph)}
+    out["gpu_v1_phase_calls"] = calls
+    nl = np.zeros(2)
+    lib.ssnt_diag_null_launch(n, nl.ctypes.data)
+    out["null_kernel_launch_us"], out["null_kernel_sync_us"] = float(nl[0]), float(nl[1])
+    return out
+
+
 def main():
     lib = _lib.load()
     lib.ssnt_set_host_staging.restype = ctypes.c_int
@@ -63,6 +105,7 @@ def main():
         lambda: O.v2_step(c2["h"], c2["hist"], c2["fin"], c2["total"], c2["table"], c2["t"],
                           c2["u"], c2["input_length"], np.zeros(64, np.int32), 0, False, True),
         n=500)
+    res.update(raw_v1(lib, c))
     big = {k: np.repeat(v, 4096, axis=0) if isinstance(v, np.ndarray) and v.ndim >= 1 else v
            for k, v in c.items()}
     t = per_call(lambda: O.v1_step(big["h"], big["hist"], big["fin"], big["t"], big["u"],
