@@ -54,6 +54,10 @@ struct HostCtx {
   size_t dcap = 0;
   char* h = nullptr;
   size_t hcap = 0;
+  char* hmap = nullptr;       // device address of the pinned staging buffer (zero-copy plans)
+  unsigned* flag_h = nullptr;  // completion word in coherent pinned memory (host side) ...
+  unsigned* flag_d = nullptr;  // ... and its device address
+  unsigned seq = 0;            // last completion value requested
 };
 thread_local HostCtx g_ctx;
 
@@ -77,11 +81,24 @@ int ctx_ready(const char* fn, bool abort_on_error) {
     }
     if (g_ctx.d) (void)hipFree(g_ctx.d);
     if (g_ctx.h) (void)hipHostFree(g_ctx.h);
+    if (g_ctx.flag_h) (void)hipHostFree(g_ctx.flag_h);
     g_ctx = HostCtx{};
     g_ctx.device = dev;
     if (hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking) != hipSuccess) {
       if (abort_on_error) fail(fn, "hipStreamCreate failed");
       return SSNT_ERR_HIP;
+    }
+    // the completion word of the per-step symbols: coherent (uncached) pinned memory, so a GPU
+    // write of it is visible to the polling host thread without a cache flush
+    void* fh = nullptr;
+    void* fd = nullptr;
+    if (hipHostMalloc(&fh, 4096, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
+        hipHostGetDevicePointer(&fd, fh, 0) == hipSuccess && fd) {
+      g_ctx.flag_h = static_cast<unsigned*>(fh);
+      g_ctx.flag_d = static_cast<unsigned*>(fd);
+      *g_ctx.flag_h = 0;
+    } else if (fh) {
+      (void)hipHostFree(fh);
     }
   }
   return SSNT_OK;
@@ -108,6 +125,7 @@ int ensure(size_t dbytes, size_t hbytes, const char* fn, bool abort_on_error) {
       (void)hipHostFree(g_ctx.h);
     }
     g_ctx.h = nullptr;
+    g_ctx.hmap = nullptr;
     g_ctx.hcap = 0;
     const size_t cap = hbytes + hbytes / 2 + 4096;
     if (hipHostMalloc(reinterpret_cast<void**>(&g_ctx.h), cap, hipHostMallocDefault) != hipSuccess) {
@@ -139,6 +157,38 @@ struct PhaseClock {
   }
 };
 thread_local PhaseClock g_clk;
+
+// How a per-step call (zero-copy plan) learns that its kernel is done: 0 hipStreamSynchronize;
+// 1 hipStreamWriteValue32 of a sequence number into a coherent pinned word after the kernel,
+// polled by the calling thread; 2 the same word written by a one-thread kernel launched after
+// it. A poll that sees nothing for kFlagTimeoutMs falls back to hipStreamSynchronize (which
+// then reports a failed kernel). Default measured per DESIGN.md 7.2 (tools/bench_step_symbols.py).
+std::atomic<int> g_sync_mode{2};
+constexpr double kFlagTimeoutMs = 5000.0;
+
+__global__ void k_flag(unsigned* f, unsigned v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// enqueue the completion write behind the calling thread's kernels and spin until it lands;
+// false: not seen (the caller synchronises)
+bool wait_flag(int mode) {
+  const unsigned seq = ++g_ctx.seq;
+  if (mode == 1) {
+    if (hipStreamWriteValue32(g_ctx.stream, g_ctx.flag_d, seq, 0) != hipSuccess) return false;
+  } else {
+    hipLaunchKernelGGL(k_flag, dim3(1), dim3(1), 0, g_ctx.stream, g_ctx.flag_d, seq);
+    if (hipGetLastError() != hipSuccess) return false;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned long n = 0;; ++n) {
+    if (__atomic_load_n(g_ctx.flag_h, __ATOMIC_ACQUIRE) == seq) return true;
+    if ((n & 1023) == 1023 &&
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > kFlagTimeoutMs)
+      return false;
+    __builtin_ia32_pause();
+  }
+}
 
 // Host staging mode for the small per-step reference symbols (not ssnt_fwd_bwd, whose tensors
 // are large): 0 = one H2D copy of inputs + zeroed status word, kernel, one D2H copy; 1 =
@@ -196,13 +246,15 @@ int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device =
                   abort_on_error);
   if (rc != SSNT_OK) return rc;
   if (p.zero_copy) {
-    void* mapped = nullptr;
-    if (hipHostGetDevicePointer(&mapped, g_ctx.h, 0) != hipSuccess || mapped == nullptr) {
+    void* mapped = g_ctx.hmap;  // looked up once per staging allocation
+    if (!mapped && (hipHostGetDevicePointer(&mapped, g_ctx.h, 0) != hipSuccess || mapped == nullptr)) {
+      mapped = nullptr;
       p.zero_copy = false;  // not mappable here: fall back to the copies
       rc = ensure(Plan::align(p.total) + extra_device, p.total, fn, abort_on_error);
       if (rc != SSNT_OK) return rc;
     } else {
-      p.dbase = static_cast<char*>(mapped);
+      g_ctx.hmap = static_cast<char*>(mapped);
+      p.dbase = g_ctx.hmap;
     }
   }
   if (!p.zero_copy) p.dbase = g_ctx.d;
@@ -240,7 +292,11 @@ int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
     const size_t lo = p.status_off, hi = p.total;
     e = hipMemcpyAsync(g_ctx.h + lo, g_ctx.d + lo, hi - lo, hipMemcpyDeviceToHost, g_ctx.stream);
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(g_ctx.stream);
+  const int sync_mode = g_sync_mode.load(std::memory_order_relaxed);
+  if (e == hipSuccess && p.zero_copy && sync_mode != 0 && g_ctx.flag_h && wait_flag(sync_mode))
+    ;  // completion seen through the flag word: the outputs are in the staging buffer
+  else if (e == hipSuccess)
+    e = hipStreamSynchronize(g_ctx.stream);
   if (e != hipSuccess) {
     if (abort_on_error) fail(fn, hipGetErrorString(e));
     return SSNT_ERR_HIP;
@@ -532,6 +588,13 @@ int ssnt_fwd_bwd_last_kernel(char* buf, size_t len) {
 int ssnt_set_host_staging(int mode) {
   if (mode != 0 && mode != 1) return -1;
   return g_host_mode.exchange(mode);
+}
+
+// A/B of how the per-step reference symbols wait for their kernel (g_sync_mode); not part of
+// the public header. Returns the previous mode.
+int ssnt_set_host_sync(int mode) {
+  if (mode < 0 || mode > 2) return -1;
+  return g_sync_mode.exchange(mode);
 }
 
 // A/B of the fused decodes' step ordering (tools, tests): -1 default, 0 full rank, 1 selection;

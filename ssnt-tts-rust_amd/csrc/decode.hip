@@ -8,6 +8,8 @@
 // Rust step (and with oracle/ssnt_oracle.c) by construction.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "decode_dev.h"
 
 namespace ssnt {
@@ -203,8 +205,17 @@ int launch_decode_step(const StepArgs& a, hipStream_t st) {
   const size_t n = (size_t)a.W * a.C;
   const size_t lds = n * sizeof(Cand) + 2 * n * sizeof(int);
   if (lds > 150 * 1024) return SSNT_ERR_UNSUPPORTED;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_decode_step),
-                      hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  if (lds > 64 * 1024) {  // (the attribute is per device: set once per device, not per call)
+    static std::atomic<unsigned long long> set_on{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (!(set_on.load(std::memory_order_relaxed) & bit)) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_decode_step),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      set_on.fetch_or(bit);
+    }
+  }
   hipLaunchKernelGGL(k_decode_step, dim3(a.B), dim3(64), lds, st, a);
   return last_error();
 }

@@ -34,7 +34,7 @@ namespace {
 
 using namespace dec;
 
-constexpr int kAhead = 4;    // input rows in flight
+constexpr int kAhead = 8;    // input rows in flight
 
 // Diagnostic build only (-DSSNT_DIAG, `make lib-diag`): s_memtime cycle totals of the register
 // kernel's step phases for utterance 0 (tools/diag_decode.py): 0 candidate generation, 1 rank /
@@ -253,7 +253,11 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       valid = 1; code = i; lp = hist + row[0]; nt = bt + 1; nu = bu + 1; fin = 0;
     } else {  // v2: src/v2.rs:119-166, 326-336
       tot = (int)((unsigned)btot + (unsigned)dur);
-      const u64 t = as_usize(bt);
+      // a defined beam (the only kind whose candidate is used) has t == s: every beam starts at
+      // t = 0, an unfinished candidate of a defined beam moves to t + 1, and every other
+      // candidate is finished (never defined again) -- so the band of src/v2.rs:94-111 is
+      // uniform per step
+      const u64 t = (u64)s;
       const float diagonal = o_over_i * (float)(t + 1);
       const int lb = f2i_sat(fmaxf(diagonal - lower_range, 0.0f));
       const int ub = f2i_sat(fminf(diagonal + upper_range, (float)O));

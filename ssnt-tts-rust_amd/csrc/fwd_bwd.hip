@@ -351,14 +351,16 @@ const char* last_fwd_bwd_dispatch() { return t_dispatch; }
 
 size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
   // 0 when the default dispatch keeps every row in LDS whatever the call brings: U <= 256, the
-  // streaming kernel's rows fit beside its rings even with log_obs (the larger ring slots) and
-  // the narrow form's padded rows, and the two-wave kernel (what takes 4-byte-aligned tensors)
+  // streaming kernel's rows fit beside its rings with or without log_obs and with the narrow
+  // form's padded rows, and the two-wave kernel (what takes 4-byte-aligned tensors)
   // fits its rows too. (The segmented kernel, variant 2, always needs the workspace.)
   if (variant() != 2 && U <= 256) {
     const int K = U <= 64 ? 1 : U <= 128 ? 2 : 4;
     const size_t Up = (size_t)K * ((U + K - 1) / K);
     const size_t rows = (size_t)T * Up * sizeof(xf);
-    const bool stream_lds = stream_head_bytes(K, U, true) + rows <= kLdsBudget;
+    // (log_obs rings carry wider slots, the ones without more of them: take the larger head)
+    const size_t h0 = stream_head_bytes(K, U, false), h1 = stream_head_bytes(K, U, true);
+    const bool stream_lds = (h0 > h1 ? h0 : h1) + rows <= kLdsBudget;
     const bool simple_lds = (size_t)(64 * K + 2) * sizeof(xf) + (size_t)T * U * sizeof(xf) <= kLdsBudget;
     if (stream_lds && simple_lds) return 0;
   }

@@ -334,7 +334,7 @@ __device__ __forceinline__ void lds_xrow_st(xf* p, const XRow<K>& r) {
 }
 
 // Global accesses of a lane's K positions, F floats per position. NV (narrow): one access per
-// position -- U % K != 0 or 8-byte-aligned tensors: a slice may straddle the row end, and each
+// position -- U % K != 0 or tensors aligned to 8 or 4 bytes: a slice may straddle the row end, and each
 // position is then entirely inside the row's buffer range or entirely outside it (reads 0,
 // stores dropped). Otherwise one vector access per slice.
 template <int K, int F, bool NV>
@@ -1027,11 +1027,13 @@ int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
 template <int K, bool OBS, int NC, int NH, int RS = 0>
 int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
   // whole lane slices and 16-byte aligned tensors: the vector form; else (U % K != 0, or
-  // tensors at 8-byte (trans, grad) / 4-byte (the rest) alignment) the narrow form
+  // tensors at 4-byte alignment) the narrow form: one 8-byte access per (emit, shift) position,
+  // which buffer loads and stores take at any dword alignment (a sliced log_trans / grad at an
+  // odd float offset no longer drops to the two-wave kernel)
   const bool vec = (a.U % K == 0) && aligned16(a.log_trans) && aligned16(a.log_obs) &&
                    aligned16(a.grad) && aligned16(a.grad_obs) && aligned16(a.log_alpha) &&
                    aligned16(a.log_beta) && aligned16(a.workspace);
-  const bool narrow_ok = aligned_to(a.log_trans, 8) && aligned_to(a.grad, 8) && aligned16(a.workspace) &&
+  const bool narrow_ok = aligned_to(a.log_trans, 4) && aligned_to(a.grad, 4) && aligned16(a.workspace) &&
                          aligned_to(a.log_obs, 4) && aligned_to(a.grad_obs, 4) &&
                          aligned_to(a.log_alpha, 4) && aligned_to(a.log_beta, 4);
   if (!vec && !narrow_ok) return SSNT_ERR_UNSUPPORTED;

@@ -35,8 +35,15 @@ namespace {
 // steps per hand-off block = rows in flight per wave (ring indices static). At K = 1, 16 rows of
 // 512 B per wave keep ~2 us of HBM latency covered at a ~0.2 us step (Little's law: 8 rows held
 // the kernel near 3 TB/s); K = 2 has twice the bytes per row and the registers for 8.
-template <int K>
-constexpr int block_steps() { return K == 1 ? 16 : 8; }
+// (build-time overrides for tuning studies: SSNT_W_D1 / SSNT_W_D2, phase 1 / 2 at K = 1)
+#ifndef SSNT_W_D1
+#define SSNT_W_D1 16
+#endif
+#ifndef SSNT_W_D2
+#define SSNT_W_D2 16
+#endif
+template <int K, int PHASE>
+constexpr int block_steps() { return K == 1 ? (PHASE == 1 ? SSNT_W_D1 : SSNT_W_D2) : 8; }
 constexpr int kRB = 64;        // hand-off ring slots (steps) per wave
 constexpr int kMaxNW = 8;      // waves per direction: U <= 512 (K = 1) / 1024 (K = 2)
 constexpr int kSpinMax = 1 << 22;
@@ -106,7 +113,8 @@ struct WRows {    // phase-2 workspace rows for this lane
 template <int K, bool OBS, int PHASE, bool DBG>
 __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   constexpr int kSeg = 64 * K;
-  constexpr int kBS = block_steps<K>();
+  constexpr int kBS = block_steps<K, PHASE>();
+  static_assert(kRB % kBS == 0, "hand-off blocks must tile the ring");
   constexpr int kDepth = kBS;  // rows in flight per wave
   __shared__ WideCtl ctl;
   const int b = blockIdx.x;

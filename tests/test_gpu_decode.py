@@ -37,6 +37,21 @@ def select_mode(request, gpu):
     lib.ssnt_fused_decode_select(-1)
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["sync", "writevalue", "flagkernel"])
+def host_sync(request, gpu):
+    """The per-step host symbols' three ways of waiting for their kernel (hipStreamSynchronize,
+    a hipStreamWriteValue32 completion word, a completion word written by a flag kernel) must
+    return identical outputs."""
+    import ctypes
+    lib = gpu.load()
+    lib.ssnt_set_host_sync.restype = ctypes.c_int
+    lib.ssnt_set_host_sync.argtypes = [ctypes.c_int]
+    prev = lib.ssnt_set_host_sync(request.param)
+    assert prev >= 0
+    yield request.param
+    lib.ssnt_set_host_sync(prev)
+
+
 V1_KEYS = ("prediction", "log_prob", "next_t", "next_u", "next_is_finished", "beam_branch")
 V2_KEYS = ("prediction", "log_prob", "next_t", "next_u", "next_is_finished",
            "next_total_duration", "beam_branch")
@@ -88,7 +103,7 @@ def test_v2_step(gpu, oracle, seed):
 
 
 @pytest.mark.parametrize("seed", range(40))
-def test_reference_host_symbols_v1(gpu, oracle, seed):
+def test_reference_host_symbols_v1(gpu, oracle, seed, host_sync):
     # the exact ABI the TF op binds: ssnt_tts_beam_search_decode, batch fixed to 1
     from ssnt_tts_amd import capi
     c = dc.v1_case(seed, B=1)
@@ -100,7 +115,7 @@ def test_reference_host_symbols_v1(gpu, oracle, seed):
 
 
 @pytest.mark.parametrize("seed", range(40))
-def test_reference_host_symbols_v2_tone(gpu, oracle, seed):
+def test_reference_host_symbols_v2_tone(gpu, oracle, seed, host_sync):
     from ssnt_tts_amd import capi
     c = dc.v2_case(seed)
     B, W, D = c["h"].shape
@@ -164,7 +179,7 @@ def test_order_beam_branch(gpu, oracle, shape):
     assert np.array_equal(capi.ssnt_order_beam_branch(fb, bb, B, W, T), want)
 
 
-def test_upsample_known_answer_and_random(gpu, oracle, golden):
+def test_upsample_known_answer_and_random(gpu, oracle, golden, host_sync):
     from ssnt_tts_amd import capi
     fx = golden["upsample_source_indexes"]
     d = np.array(fx["duration"], np.int32)
@@ -265,7 +280,7 @@ def test_lattice_decode_paths(gpu, oracle, shape, tie_rich, select_mode):
         assert np.array_equal(got[k].cpu().numpy(), v), k
 
 
-def test_v1_seven_step_reference_sequence(gpu, oracle, golden):
+def test_v1_seven_step_reference_sequence(gpu, oracle, golden, host_sync):
     # ssnt-tts-tensorflow/tests/test_beam_search_op.py:11-34: the reference's only multi-step v1
     # op sequence (W=3, max_t=4), fed step by step through the exact symbol the TF op binds
     # (ssnt_tts_beam_search_decode, host pointers, batch 1) and through the batched device entry;

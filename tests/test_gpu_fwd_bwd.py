@@ -289,6 +289,21 @@ def test_fused_loss_sum_more_workgroups_than_cus(gpu, oracle, kernel_variant):
         assert r["loss_sum"].cpu().numpy()[0] == _wave_order_sum(o["loss"])
 
 
+@pytest.mark.parametrize("U", [79, 81, 127])
+@pytest.mark.parametrize("obs", [False, True])
+def test_lds_edge_rows_without_workspace_query_mismatch(gpu, oracle, U, obs):
+    # T*U rows near the LDS budget with U % K != 0 (the narrow form pads rows) at T=200: the
+    # workspace the library asks for must cover the kernel it then dispatches (with and without
+    # log_obs, whose rings differ)
+    B, T = 3, 200
+    lt = oracle.synth_log_trans(B, T, U, seed=U)
+    lo = (np.random.default_rng(U).standard_normal((B, T, U)) * 15 - 40).astype(np.float32) if obs else None
+    S, P = [T, 150, 120], [U, U - 7, 40]
+    g = _run_gpu(gpu, lt, S, P, lo, debug=False)
+    o = oracle.fwd_bwd_xf(lt, S, P, log_obs=lo)
+    _assert_bit_exact(g, o, ["loss", "grad"] + (["grad_obs"] if obs else []))
+
+
 _C3 = {}
 
 
@@ -356,9 +371,9 @@ def test_rows_beyond_512_bit_exact(gpu, oracle, kernel_variant, shape):
 @pytest.mark.parametrize("shift", [1, 2, 4])
 @pytest.mark.parametrize("U", [80, 81, 127, 33])
 def test_offset_and_odd_shapes(gpu, oracle, kernel_variant, shift, U):
-    # tensors at an element offset (4 / 8 / 16-byte aligned bases) and U % K != 0: the streaming
-    # kernel's narrow form takes U % K != 0 and 8-byte alignment, the two-wave kernel 4-byte
-    # alignment -- with identical bits
+    # log_trans AND grad at an element offset (4 / 8 / 16-byte aligned bases) and U % K != 0:
+    # the streaming kernel's narrow form takes U % K != 0 and 4- or 8-byte alignment (one 8-byte
+    # access per position), its vector form 16-byte alignment -- with identical bits
     dev = torch.device("cuda:0")
     B, T = 5, max(90, U + 10)
     lt = oracle.synth_log_trans(B, T, U, seed=shift + U)
@@ -369,9 +384,16 @@ def test_offset_and_odd_shapes(gpu, oracle, kernel_variant, shift, U):
     flat[shift:] = torch.from_numpy(lt.ravel()).to(dev)
     x = flat[shift:].view(B, T, U, 2)
     assert x.data_ptr() % 16 == (4 * shift) % 16
+    gflat = torch.full((lt.size + shift,), 7.0, dtype=torch.float32, device=dev)
+    gv = gflat[shift:].view(B, T, U, 2)
     r = gpu.ssnt_fwd_bwd(x, torch.tensor(S, dtype=torch.int32, device=dev),
-                         torch.tensor(P, dtype=torch.int32, device=dev), debug=True, check=True)
+                         torch.tensor(P, dtype=torch.int32, device=dev), debug=True, check=True,
+                         out={"grad": gv})
+    if kernel_variant == 0 and shift % 4:  # the default dispatch keeps the streaming kernel
+        assert gpu.last_fwd_bwd_kernel().startswith("k_fwd_bwd_stream<"), gpu.last_fwd_bwd_kernel()
+        assert "NV=1" in gpu.last_fwd_bwd_kernel()
     g = {k: v.cpu().numpy() for k, v in r.items() if k != "status"}
+    assert gflat[:shift].eq(7.0).all()  # nothing written before the view
     o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
     _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
 

@@ -106,6 +106,17 @@ def main():
                           c2["u"], c2["input_length"], np.zeros(64, np.int32), 0, False, True),
         n=500)
     res.update(raw_v1(lib, c))
+    lib.ssnt_set_host_sync.restype = ctypes.c_int
+    lib.ssnt_set_host_sync.argtypes = [ctypes.c_int]
+    prev = lib.ssnt_set_host_sync(0)
+    for mode in (0, 1, 2):  # completion: hipStreamSynchronize / hipStreamWriteValue32 / flag kernel
+        lib.ssnt_set_host_sync(mode)
+        r = raw_v1(lib, c, n=3000)
+        res[f"sync{mode}_raw_gpu_v1_W4_us"] = r["raw_gpu_v1_W4_us"]
+        res[f"sync{mode}_gpu_v1_phase_us"] = r["gpu_v1_phase_us"]
+        res[f"sync{mode}_gpu_v1_W4_us_wrapped"] = per_call(v1)
+        res[f"sync{mode}_gpu_v2_B64_W4_D16_us_wrapped"] = per_call(v2, n=500)
+    lib.ssnt_set_host_sync(prev)
     big = {k: np.repeat(v, 4096, axis=0) if isinstance(v, np.ndarray) and v.ndim >= 1 else v
            for k, v in c.items()}
     t = per_call(lambda: O.v1_step(big["h"], big["hist"], big["fin"], big["t"], big["u"],
