@@ -49,6 +49,16 @@ lib-exp: $(EXPDIR)/libssnt_tts_c.so
 $(EXPDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -DSSNT_DIAG -DSSNT_EXP -c $< -o $@
+# experiment build without the diagnostic stamps (kernel time of SSNT_EXP masks, tools/ab_exp.py)
+EXPNDIR   := $(LIBDIR)/expnd
+EXPN_OBJS := $(patsubst $(CSRC)/%.hip,$(EXPNDIR)/obj/%.o,$(HIP_SRCS))
+lib-expnd: $(EXPNDIR)/libssnt_tts_c.so
+$(EXPNDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DSSNT_EXP -c $< -o $@
+$(EXPNDIR)/libssnt_tts_c.so: $(EXPN_OBJS)
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(EXPN_OBJS) -Wl,-soname,libssnt_tts_c.so
+
 $(EXPDIR)/libssnt_tts_c.so: $(EXP_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(EXP_OBJS) -Wl,-soname,libssnt_tts_c.so
 
@@ -59,4 +69,4 @@ $(ORACLE): oracle/ssnt_oracle.c
 clean:
 	rm -rf $(LIBDIR) oracle/build
 
-.PHONY: all lib lib-diag lib-exp oracle clean
+.PHONY: all lib lib-diag lib-exp lib-expnd oracle clean

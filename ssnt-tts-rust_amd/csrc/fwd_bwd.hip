@@ -354,7 +354,7 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
   // streaming kernel's rows fit beside its rings with or without log_obs and with the narrow
   // form's padded rows, and the two-wave kernel (what takes 4-byte-aligned tensors)
   // fits its rows too. (The segmented kernel, variant 2, always needs the workspace.)
-  if (variant() != 2 && U <= 256) {
+  if (variant() != 2 && stream_ring() == 0 && U <= 256) {
     const int K = U <= 64 ? 1 : U <= 128 ? 2 : 4;
     const size_t Up = (size_t)K * ((U + K - 1) / K);
     const size_t rows = (size_t)T * Up * sizeof(xf);

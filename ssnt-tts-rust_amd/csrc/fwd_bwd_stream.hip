@@ -467,6 +467,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   Diag dg;
 
   if (EXP(7) && role.kind != 1) return;  // experiment: converters alone
+  if (EXP(12) && role.kind != 0) return;  // experiment: chains alone (with 3, 10, 11: no waits)
   if (role.kind == 2) {
     // =============================== gradient waves ======================================
     const int d = role.d;
@@ -1025,7 +1026,7 @@ int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
 }
 
 template <int K, bool OBS, int NC, int NH, int RS = 0>
-int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
+int launch_stream_k(const FwdBwdArgs& a, hipStream_t st, bool force_ws = false) {
   // whole lane slices and 16-byte aligned tensors: the vector form; else (U % K != 0, or
   // tensors at 4-byte alignment) the narrow form: one 8-byte access per (emit, shift) position,
   // which buffer loads and stores take at any dword alignment (a sliced log_trans / grad at an
@@ -1041,7 +1042,7 @@ int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
   const size_t head = stream_head_bytes(K, a.U, OBS, RS);
   if (head > kLdsBudget) return SSNT_ERR_UNSUPPORTED;
   const size_t rows = (size_t)a.T * (vec ? a.U : Up) * sizeof(xf);
-  const bool lds = head + rows <= kLdsBudget;
+  const bool lds = !force_ws && head + rows <= kLdsBudget;
   if (!lds && (a.workspace == nullptr || a.workspace_bytes < (size_t)a.B * rows))
     return SSNT_ERR_WORKSPACE;
   if (vec)
@@ -1050,6 +1051,8 @@ int launch_stream_k(const FwdBwdArgs& a, hipStream_t st) {
   return lds ? launch_stream_kernel<K, OBS, true, NC, NH, RS, true>(a, head + rows, st)
              : launch_stream_kernel<K, OBS, false, NC, NH, RS, true>(a, head, st);
 }
+
+std::atomic<int> g_ring{0};  // A/B: 0 default rings; 16 / 32 ring slots with workspace rows (K = 2)
 
 template <bool OBS>
 int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
@@ -1060,6 +1063,11 @@ int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
   return launch_stream_k<2, false, 3, 4>(a, st);
 #else
   if (a.U <= 64) return launch_stream_k<1, OBS, 3, 4>(a, st);
+  if constexpr (!OBS) {  // A/B (ssnt_fwd_bwd_stream_ring): deeper rings, rows in the workspace
+    const int ring = g_ring.load(std::memory_order_relaxed);
+    if (a.U > 64 && a.U <= 128 && ring == 16) return launch_stream_k<2, false, 3, 4, 16>(a, st, true);
+    if (a.U > 64 && a.U <= 128 && ring == 32) return launch_stream_k<2, false, 3, 4, 32>(a, st, true);
+  }
   if (a.U <= 128) return launch_stream_k<2, OBS, SSNT_T_NC, SSNT_T_NH>(a, st);
   if (a.U <= 256) return launch_stream_k<4, OBS, 2, 2>(a, st);
   // K = 8 (U <= 512, configs[4]): the two-wave kernel. The streaming kernel needs 4-slot rings to
@@ -1118,6 +1126,13 @@ int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
 #endif
   return a.log_obs ? launch_stream_obs<true>(a, st) : launch_stream_obs<false>(a, st);
 }
+
+int set_stream_ring(int r) {
+  if (r != 0 && r != 16 && r != 32) return SSNT_ERR_INVALID_ARG;
+  g_ring.store(r);
+  return SSNT_OK;
+}
+int stream_ring() { return g_ring.load(std::memory_order_relaxed); }
 
 void set_stream_mix(int m) {
 #ifdef SSNT_EXP

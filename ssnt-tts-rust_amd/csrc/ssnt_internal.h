@@ -44,6 +44,8 @@ int set_fwd_bwd_variant(int v);
 // streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t stream);
 void set_stream_mix(int m);  // tuning only
+int set_stream_ring(int r);  // A/B only: 0 default, 16 / 32 ring slots with workspace rows
+int stream_ring();
 // segmented kernel (fwd_bwd_wide.hip): long rows (256 < U <= 1024), or any U <= 1024 when
 // any_u; SSNT_ERR_UNSUPPORTED for other shapes
 int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t stream, bool any_u);

@@ -96,6 +96,14 @@ def _bench_worker(rank, world, port, q):
 
     elapsed = bench.timed_region(replay, sums, lambda x: torch.distributed.all_reduce(x),
                                  lambda: None, torch.distributed.barrier)
+    sums2 = torch.zeros(K)
+
+    def step_k(k):  # bench's per-step form: one step, then its own all-reduce
+        sums2[k] = float(O.fwd_bwd_xf(lt, [T] * (hi - lo), [U] * (hi - lo))["loss"].sum())
+        torch.distributed.all_reduce(sums2[k:k + 1])
+
+    bench.per_step_region(step_k, K, lambda: None, torch.distributed.barrier)
+    assert torch.equal(sums2, sums)  # the same reduced per-step sums either way
     t = torch.tensor([elapsed], dtype=torch.float64)
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     line = bench.result_line(world, hi - lo, T, U, K, 0, float(t[0]), 0.01, True)

@@ -439,3 +439,27 @@ def test_rows_beyond_512_live_ragged_batch(gpu, oracle, wide_lanes, kernel_varia
     g = _run_gpu(gpu, lt, S, P)
     o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
     _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+
+
+@pytest.mark.parametrize("ring", [16, 32])
+def test_stream_ring_depth_variants(gpu, oracle, kernel_variant, ring):
+    # the streaming kernel's deeper-ring A/B form (16 / 32 factor slots, rows in the workspace)
+    # must be bit-identical to the oracle (ragged batch, debug rows)
+    if kernel_variant != 0:
+        pytest.skip("a streaming-kernel form")
+    import ctypes
+    lib = gpu.load()
+    lib.ssnt_fwd_bwd_stream_ring.restype = ctypes.c_int
+    assert lib.ssnt_fwd_bwd_stream_ring(ring) == 0
+    try:
+        rng = np.random.default_rng(ring)
+        B, T, U = 6, 200, 80
+        lt = oracle.synth_log_trans(B, T, U, seed=ring)
+        P = [U] + [int(x) for x in rng.integers(1, U + 1, size=B - 1)]
+        S = [T] + [int(rng.integers(p, T + 1)) for p in P[1:]]
+        g = _run_gpu(gpu, lt, S, P)
+        assert f"RS={ring}" in gpu.last_fwd_bwd_kernel() and "LDS=0" in gpu.last_fwd_bwd_kernel()
+        o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
+        _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+    finally:
+        lib.ssnt_fwd_bwd_stream_ring(0)
