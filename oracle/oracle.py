@@ -19,6 +19,7 @@ _lib = None
 
 FLAG_TERMINAL_EMIT = 1
 FLAG_ZERO_INFINITY = 2
+ORACLE_PAIR = 1 << 16  # oracle-only: the pair kernel's recurrence (ssnt_oracle.c)
 
 _f32p = ctypes.POINTER(ctypes.c_float)
 _f64p = ctypes.POINTER(ctypes.c_double)
@@ -232,8 +233,12 @@ def tone_lattice_decode(logits, input_length, empty_tone_id, n_threads=0):
 
 
 def fwd_bwd_xf(log_trans, step_len, pos_len, log_obs=None, flags=FLAG_TERMINAL_EMIT,
-               debug=False, n_threads=0):
-    """Exact split-exponent f32 fwd-bwd (the arithmetic the HIP kernel reproduces bit-exactly)."""
+               debug=False, n_threads=0, pair=False):
+    """Exact split-exponent f32 fwd-bwd (the arithmetic the HIP kernel reproduces bit-exactly).
+    pair=True: the pair recurrence of the pair kernel (csrc/fwd_bwd_pair.hip, no log_obs)."""
+    if pair:
+        assert log_obs is None, "the pair recurrence has no log_obs form"
+        flags = int(flags) | ORACLE_PAIR
     lt = _f32(log_trans)
     B, T, U, _ = lt.shape
     lo = None if log_obs is None else _f32(log_obs)

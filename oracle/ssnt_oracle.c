@@ -611,6 +611,10 @@ int oracle_tone_lattice_decode(int B, int T, int W, int C, const float *logits,
  * ========================================================================================== */
 #define FLAG_TERMINAL_EMIT 1
 #define FLAG_ZERO_INFINITY 2
+/* internal (oracle only, never a kernel flag): the pair recurrence of the pair kernel
+ * (csrc/fwd_bwd_pair.hip). Even rows advance two steps at a time, odd rows are one
+ * step from the even row before them, the cut is even. No log_obs. */
+#define ORACLE_PAIR (1 << 16)
 
 /* --- split-exponent ("xf") f32 arithmetic: value = m * 2^e ------------------------------- */
 typedef struct { float m; int32_t e; } xf;
@@ -674,6 +678,70 @@ static inline xf xf_add(float ma, int32_t ea, float mb, int32_t eb) {
 
 static inline float xf_neg_post(float m, int32_t e) { return 0.0f - ldexpf(m, e); }
 
+/* ---- pair recurrence (ORACLE_PAIR; csrc/fwd_bwd_pair.hip) ------------------------------------
+ * Two steps of the emit/shift recurrence composed into one: with factors E, Sh of rows s and
+ * s+1 (primed), alpha[s+2][p] = c0 a[p] + c1 a[p-1] + c2 a[p-2] (a = alpha[s]) and
+ * beta[s][p] = d0 b[p] + d1 b[p+1] + d2 b[p+2] (b = beta[s+2]), where
+ *   c0 = E E'              c1 = Sh[p-1] E'[p] (+) E[p-1] Sh'[p-1]    c2 = Sh[p-2] Sh'[p-1]
+ *   d0 = E E'              d1 = E[p] Sh'[p] (+) Sh[p] E'[p+1]        d2 = Sh[p] Sh'[p+1]
+ * (products unnormalized, (+) = xf_add). The three terms are summed in order (t0 + t1) + t2
+ * after aligning to the exponent max clamped at XF_EZERO, then normalized. */
+static const xf XF_Z = {0.0f, XF_EZERO};
+static inline xf xf_mul(xf a, xf b) { return (xf){a.m * b.m, a.e + b.e}; }
+static inline xf xf_sum3(xf t0, xf t1, xf t2) {
+    int32_t em = t0.e > t1.e ? t0.e : t1.e;
+    em = em > t2.e ? em : t2.e;
+    em = em > XF_EZERO ? em : XF_EZERO;
+    const float s = (ldexpf(t0.m, t0.e - em) + ldexpf(t1.m, t1.e - em)) + ldexpf(t2.m, t2.e - em);
+    return xf_norm(s, em);
+}
+/* one forward step from row s (the oracle's single-step alpha, no log_obs) */
+static void step_fwd(const xf *a, const xf *E, const xf *Sh, int U, xf *out) {
+    for (int p = 0; p < U; ++p) {
+        const float sm = a[p].m * E[p].m;
+        const int32_t se = a[p].e + E[p].e;
+        float hm = 0.0f;
+        int32_t he = XF_EZERO;
+        if (p > 0) {
+            hm = a[p - 1].m * Sh[p - 1].m;
+            he = a[p - 1].e + Sh[p - 1].e;
+        }
+        const int32_t em = se > he ? se : he;
+        out[p] = xf_norm(ldexpf(sm, se - em) + ldexpf(hm, he - em), em);
+    }
+}
+/* one backward step into row s from b = beta[s+1] */
+static void step_bwd(const xf *b, const xf *E, const xf *Sh, int U, xf *out) {
+    for (int p = 0; p < U; ++p) {
+        const xf q = b[p], r = (p + 1 < U) ? b[p + 1] : XF_Z;
+        out[p] = xf_add(E[p].m * q.m, E[p].e + q.e, Sh[p].m * r.m, Sh[p].e + r.e);
+    }
+}
+static void pair_fwd(const xf *a, const xf *E, const xf *Sh, const xf *E1, const xf *Sh1, int U, xf *out) {
+    for (int p = 0; p < U; ++p) {
+        const xf c0 = xf_mul(E[p], E1[p]);
+        xf c1 = XF_Z, c2 = XF_Z;
+        if (p >= 1) {
+            const xf ta = xf_mul(Sh[p - 1], E1[p]), tb = xf_mul(E[p - 1], Sh1[p - 1]);
+            c1 = xf_add(ta.m, ta.e, tb.m, tb.e);
+        }
+        if (p >= 2) c2 = xf_mul(Sh[p - 2], Sh1[p - 1]);
+        out[p] = xf_sum3(xf_mul(a[p], c0), p >= 1 ? xf_mul(a[p - 1], c1) : XF_Z,
+                         p >= 2 ? xf_mul(a[p - 2], c2) : XF_Z);
+    }
+}
+static void pair_bwd(const xf *b, const xf *E, const xf *Sh, const xf *E1, const xf *Sh1, int U, xf *out) {
+    for (int p = 0; p < U; ++p) {
+        const xf d0 = xf_mul(E[p], E1[p]);
+        const xf ta = xf_mul(E[p], Sh1[p]);
+        const xf tb = (p + 1 < U) ? xf_mul(Sh[p], E1[p + 1]) : XF_Z;
+        const xf d1 = xf_add(ta.m, ta.e, tb.m, tb.e);
+        const xf d2 = (p + 1 < U) ? xf_mul(Sh[p], Sh1[p + 1]) : XF_Z;
+        out[p] = xf_sum3(xf_mul(b[p], d0), (p + 1 < U) ? xf_mul(b[p + 1], d1) : XF_Z,
+                         (p + 2 < U) ? xf_mul(b[p + 2], d2) : XF_Z);
+    }
+}
+
 static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S, int P,
                            int flags, float *loss, float *g, float *go, float *la, float *lb,
                            xf *A, xf *Bt, xf *E, xf *Sh, xf *O) {
@@ -697,10 +765,19 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
             Sh[c] = xf_exp(lt[c * 2 + 1], p < P - 1);
             O[c] = lo ? xf_exp(lo[c], p < P) : (xf){1.0f, 0};
         }
+    const bool pair = (flags & ORACLE_PAIR) != 0 && !lo;
     /* alpha */
     for (int p = 0; p < U; ++p) A[p] = (xf){0.0f, XF_EZERO};
     A[0] = lo ? xf_norm(O[0].m, O[0].e) : (xf){0.5f, 1};
-    for (int s = 1; s < S; ++s)
+    if (pair) {
+        for (int s = 2; s < S; s += 2)
+            pair_fwd(A + (size_t)(s - 2) * U, E + (size_t)(s - 2) * U, Sh + (size_t)(s - 2) * U,
+                     E + (size_t)(s - 1) * U, Sh + (size_t)(s - 1) * U, U, A + (size_t)s * U);
+        for (int s = 1; s < S; s += 2)
+            step_fwd(A + (size_t)(s - 1) * U, E + (size_t)(s - 1) * U, Sh + (size_t)(s - 1) * U, U,
+                     A + (size_t)s * U);
+    }
+    for (int s = 1; s < S && !pair; ++s)
         for (int p = 0; p < U; ++p) {
             const xf a = A[(size_t)(s - 1) * U + p];
             const xf e = E[(size_t)(s - 1) * U + p];
@@ -730,7 +807,23 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
         const xf e = E[(size_t)(S - 1) * U + P - 1];
         Bt[(size_t)(S - 1) * U + P - 1] = term ? xf_norm(e.m, e.e) : (xf){0.5f, 1};
     }
-    for (int s = S - 2; s >= 0; --s)
+    if (pair) {
+        /* even rows: two steps down from the even row above, or (S-1 odd) one step from beta[S-1];
+         * odd rows below S-1: one step down from the even row above */
+        for (int s = (S - 1) & ~1; s >= 0; s -= 2) {
+            if (s == S - 1) continue;
+            xf *o = Bt + (size_t)s * U;
+            if (s + 2 <= S - 1)
+                pair_bwd(Bt + (size_t)(s + 2) * U, E + (size_t)s * U, Sh + (size_t)s * U,
+                         E + (size_t)(s + 1) * U, Sh + (size_t)(s + 1) * U, U, o);
+            else
+                step_bwd(Bt + (size_t)(s + 1) * U, E + (size_t)s * U, Sh + (size_t)s * U, U, o);
+        }
+        for (int s = 1; s < S - 1; s += 2)
+            step_bwd(Bt + (size_t)(s + 1) * U, E + (size_t)s * U, Sh + (size_t)s * U, U,
+                     Bt + (size_t)s * U);
+    }
+    for (int s = S - 2; s >= 0 && !pair; --s)
         for (int p = 0; p < U; ++p) {
             xf q = Bt[(size_t)(s + 1) * U + p], r = {0.0f, XF_EZERO};
             if (p + 1 < U) r = Bt[(size_t)(s + 1) * U + p + 1];
@@ -746,7 +839,7 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
             Bt[(size_t)s * U + p] = xf_add(e.m * q.m, e.e + q.e, sh.m * r.m, sh.e + r.e);
         }
     /* Z at the cut M = (S-1)>>1: binary tree (pairs (2i,2i+1) first) over p in [0, 2^n). */
-    const int M = (S - 1) >> 1;
+    const int M = pair ? ((S - 1) >> 1) & ~1 : (S - 1) >> 1;  /* the pair kernel's cut is even */
     int n2 = 1;
     while (n2 < P) n2 <<= 1;
     xf *w = (xf *)malloc(sizeof(xf) * n2);

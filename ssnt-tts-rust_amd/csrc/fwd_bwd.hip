@@ -324,8 +324,10 @@ int launch_simple(const FwdBwdArgs& a, hipStream_t st) {
   return SSNT_ERR_UNSUPPORTED;
 }
 
-// 0 streaming kernel (fwd_bwd_stream.hip; falls back to the two-wave kernel for shapes it does
-// not take), 1 two-wave kernel only. Process-wide A/B switch: read from the environment once
+// 0 default: the pair kernel (fwd_bwd_pair.hip, U <= 128 without log_obs), else the streaming
+// kernel (fwd_bwd_stream.hip), else the segmented kernel, else the two-wave kernel; 1 two-wave
+// kernel only; 2 segmented kernel; 3 the default without the pair kernel (the one-step
+// streaming kernel). Process-wide A/B switch: read from the environment once
 // (SSNT_FWD_BWD_KERNEL=simple selects 1), atomic so concurrent callers never race on it.
 std::atomic<int> g_variant{0};
 std::once_flag g_variant_env;
@@ -362,7 +364,9 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
     const size_t h0 = stream_head_bytes(K, U, false), h1 = stream_head_bytes(K, U, true);
     const bool stream_lds = (h0 > h1 ? h0 : h1) + rows <= kLdsBudget;
     const bool simple_lds = (size_t)(64 * K + 2) * sizeof(xf) + (size_t)T * U * sizeof(xf) <= kLdsBudget;
-    if (stream_lds && simple_lds) return 0;
+    // the pair kernel (U <= 128, no log_obs) keeps half the rows beside larger rings
+    const bool pair_lds = U > 128 || pair_head_bytes(K, U) + pair_storage_bytes(K, T, U) <= kLdsBudget;
+    if (stream_lds && simple_lds && pair_lds) return 0;
   }
   // the segmented kernel keeps its rows (plus beta at the cut) in the workspace at every T; one
   // size serves every kernel variant (the two-wave kernel needs B*T*U xf at most)
@@ -376,13 +380,14 @@ int set_fwd_bwd_variant(int v) {
   // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel (fwd_bwd_wide.hip) at every U it
   // takes; 3..11 (SSNT_EXP builds only): streaming kernel with another wave mix / ring /
   // publication period (tuning)
-  if (v < 0 || v > 11) return SSNT_ERR_INVALID_ARG;
+  // takes; 12: the default without the pair kernel (one-step streaming kernel)
+  if (v < 0 || v > 12) return SSNT_ERR_INVALID_ARG;
 #ifndef SSNT_EXP
-  if (v >= 3) return SSNT_ERR_UNSUPPORTED;
+  if (v >= 3 && v != 12) return SSNT_ERR_UNSUPPORTED;
 #endif
   variant();  // the environment is read once, before any explicit choice
-  g_variant.store(v >= 3 ? 0 : v);
-  set_stream_mix(v >= 3 ? v - 2 : 0);
+  g_variant.store(v == 12 ? 3 : v >= 3 ? 0 : v);
+  set_stream_mix(v >= 3 && v != 12 ? v - 2 : 0);
   return SSNT_OK;
 }
 
@@ -394,14 +399,16 @@ __global__ __launch_bounds__(64) void k_loss_sum(const float* loss, int B, float
 
 int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
   summed = false;
-  if (variant() == 0) {
+  if (variant() == 0 || variant() == 3) {
     FwdBwdArgs x = a;
 #ifdef SSNT_EXP
     const char* ee = getenv("SSNT_EXP");
     x.exp = ee ? atoi(ee) : 0;
 #endif
     if (!a.sum_state) x.loss_sum = nullptr;
-    int rc = launch_fwd_bwd_stream(x, st);
+    int rc = SSNT_ERR_UNSUPPORTED;
+    if (variant() == 0 && stream_ring() == 0) rc = launch_fwd_bwd_pair(x, st);
+    if (rc == SSNT_ERR_UNSUPPORTED) rc = launch_fwd_bwd_stream(x, st);
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;
     summed = false;

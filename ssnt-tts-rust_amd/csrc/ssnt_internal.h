@@ -52,6 +52,10 @@ int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t stream, bool any_u);
 size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U);
 int set_fwd_bwd_wide_lanes(int k);  // A/B: positions per lane of the long-row kernel (1 or 2)
 size_t stream_head_bytes(int K, int U, bool obs, int ring = 0);  // LDS bytes besides the lattice rows
+// pair kernel (fwd_bwd_pair.hip): U <= 128 without log_obs; SSNT_ERR_UNSUPPORTED otherwise
+int launch_fwd_bwd_pair(const FwdBwdArgs& a, hipStream_t stream);
+size_t pair_head_bytes(int K, int U);            // LDS bytes besides the stored rows
+size_t pair_storage_bytes(int K, int T, int U);  // stored rows of one utterance
 int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only (tools/diag_fwd_bwd.py)
 // the fwd-bwd kernel instance this thread dispatched last ("k_fwd_bwd_stream<K=2,...>"; one
 // name per launch of a multi-launch kernel, joined by '+'); for bench.py's profile check
