@@ -324,11 +324,12 @@ int launch_simple(const FwdBwdArgs& a, hipStream_t st) {
   return SSNT_ERR_UNSUPPORTED;
 }
 
-// 0 default: the pair kernel (fwd_bwd_pair.hip, U <= 128 without log_obs), else the streaming
-// kernel (fwd_bwd_stream.hip), else the segmented kernel, else the two-wave kernel; 1 two-wave
-// kernel only; 2 segmented kernel; 3 the default without the pair kernel (the one-step
-// streaming kernel). Process-wide A/B switch: read from the environment once
-// (SSNT_FWD_BWD_KERNEL=simple selects 1), atomic so concurrent callers never race on it.
+// 0 default: the streaming kernel (fwd_bwd_stream.hip), else the segmented kernel, else the
+// two-wave kernel; 1 two-wave kernel only; 2 segmented kernel; 3 the default with the pair
+// kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs; bit-exact with the oracle's pair
+// recurrence, measured slower than the streaming kernel: DESIGN.md 5.1a). Process-wide A/B
+// switch: read from the environment once (SSNT_FWD_BWD_KERNEL=simple selects 1), atomic so
+// concurrent callers never race on it.
 std::atomic<int> g_variant{0};
 std::once_flag g_variant_env;
 int variant() {
@@ -365,7 +366,8 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
     const bool stream_lds = (h0 > h1 ? h0 : h1) + rows <= kLdsBudget;
     const bool simple_lds = (size_t)(64 * K + 2) * sizeof(xf) + (size_t)T * U * sizeof(xf) <= kLdsBudget;
     // the pair kernel (U <= 128, no log_obs) keeps half the rows beside larger rings
-    const bool pair_lds = U > 128 || pair_head_bytes(K, U) + pair_storage_bytes(K, T, U) <= kLdsBudget;
+    const bool pair_lds = variant() != 3 || U > 128 ||
+                          pair_head_bytes(K, U) + pair_storage_bytes(K, T, U) <= kLdsBudget;
     if (stream_lds && simple_lds && pair_lds) return 0;
   }
   // the segmented kernel keeps its rows (plus beta at the cut) in the workspace at every T; one
@@ -380,7 +382,7 @@ int set_fwd_bwd_variant(int v) {
   // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel (fwd_bwd_wide.hip) at every U it
   // takes; 3..11 (SSNT_EXP builds only): streaming kernel with another wave mix / ring /
   // publication period (tuning)
-  // takes; 12: the default without the pair kernel (one-step streaming kernel)
+  // takes; 12: the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs)
   if (v < 0 || v > 12) return SSNT_ERR_INVALID_ARG;
 #ifndef SSNT_EXP
   if (v >= 3 && v != 12) return SSNT_ERR_UNSUPPORTED;
@@ -407,7 +409,7 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
 #endif
     if (!a.sum_state) x.loss_sum = nullptr;
     int rc = SSNT_ERR_UNSUPPORTED;
-    if (variant() == 0 && stream_ring() == 0) rc = launch_fwd_bwd_pair(x, st);
+    if (variant() == 3 && stream_ring() == 0) rc = launch_fwd_bwd_pair(x, st);
     if (rc == SSNT_ERR_UNSUPPORTED) rc = launch_fwd_bwd_stream(x, st);
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;

@@ -40,13 +40,23 @@
 namespace ssnt {
 namespace {
 
-constexpr int kPairOut = 4;         // chain-row ring entries per direction (even rows past the cut)
+// timing-experiment knobs (tools/build_fixed.sh builds only: one mask baked in; compiled out of
+// the product): 0 gradient waves read and release but do no math, 1 converters skip exp() and
+// the coefficients, 3 chains never poll converters, 11 chains never poll releases, 12 chains
+// alone (other roles exit), 13 converters alone
+#if defined(SSNT_EXP) && defined(SSNT_EXP_FIXED)
+#define PEXP(bit) ((((SSNT_EXP_FIXED) >> (bit)) & 1) != 0)
+#else
+#define PEXP(bit) false
+#endif
+
+constexpr int kPairOut = 8;         // chain-row ring entries per direction (even rows past the cut)
 constexpr int kPairConvDepth = 4;   // pairs in flight per converter (8 log_trans rows)
 constexpr int kPairPF = 2;          // coefficient sets in flight per chain
-enum PairBlk { kC0 = 0, kC1, kC2, kE0, kX0, kE1, kX1, kNBlk };
+enum PairBlk { kC0 = 0, kC1, kC2, kNBlk };  // ring slot blocks: the chain's coefficients
 
-// ring slots (pairs) per direction: 8 (16 rows of slack) while the rings stay under ~72 KB
-__host__ __device__ constexpr int pair_slots_for(int Up) { return Up <= 80 ? 8 : 4; }
+// ring slots (pairs) per direction: 16 (32 rows of slack) while the rings stay under ~64 KB
+__host__ __device__ constexpr int pair_slots_for(int Up) { return Up <= 80 ? 16 : 8; }
 
 // x[p - O] (FWD) or x[p + O] of this lane's K positions, O = 1 or 2: own positions, the
 // neighbour lane's by one DPP, two lanes away (K = 1, O = 2) by two. Zero-filled at the wave
@@ -246,9 +256,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
   const int nstream = kmax + 1;       // converted pairs per direction
   const int nA = (S - 1) >> 1;        // alpha pair steps: alpha[2], ..., alpha[2 nA]
   // gradient pairs: forward (M+2g, M+2g+1) for g < ngf; backward (M-2g-2, M-2g-1) for g < qc;
-  // first stream index a gradient pair reads: forward qc + g, backward kmax - qc + 1 + g
   const int ngf = (S - M + 1) >> 1;
-  const int hbf = qc, hbb = kmax - qc + 1;
 
   auto row_st = [&](int idx, const XRow<K>& r) {  // storage row idx
     if constexpr (LDS) {
@@ -282,6 +290,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
   }
   __syncthreads();
   Diag dg;
+  if (PEXP(12) && role.kind != 0) return;
+  if (PEXP(13) && role.kind != 1) return;
 
   if (role.kind == 2) {
     // =============================== gradient waves ======================================
@@ -394,19 +404,23 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
       cbar();
     };
     const bool dbg = la || lb;
-    for (int i = 0; h + kNH * i < npairs; ++i) {
+    // The factors of the pair come from log_trans itself (loaded one pair ahead, converted here
+    // with the converters' own exp): the ring carries only the chain's three coefficient blocks,
+    // since LDS stores, not loads, bound the converters.
+    const int nmine = (npairs - h + kNH - 1) / kNH;
+    auto gload = [&](int i, Item<K, false>& r0, Item<K, false>& r1) {
+      const int gp = h + kNH * i;
+      const int k = d == 0 ? qc + gp : qc - 1 - gp;
+      const int row0 = min(max(2 * k, 0), T - 1), row1 = min(max(2 * k + 1, 0), T - 1);
+      gld<K, 2, NV>(r0.lt, brsrc(lt + (size_t)row0 * U * 2, U * 8u), p0);
+      gld<K, 2, NV>(r1.lt, brsrc(lt + (size_t)row1 * U * 2, U * 8u), p0);
+    };
+    auto body = [&](int i, const Item<K, false>& r0, const Item<K, false>& r1) {
       const int gp = h + kNH * i;
       if (d == 0) {
-        const int k = qc + gp;  // lattice pair (2k, 2k+1); alpha stream index k
+        const int k = qc + gp;  // lattice pair (2k, 2k+1)
         const int s0 = 2 * k, s1 = s0 + 1;
         if (gp > 0) wait_chain(qc + gp);  // alpha[s0] written by pair step qc + gp - 1
-        const xf* sl = slot_of(0, k);
-        const XRow<K> E0 = blk_ld(sl, kE0), L0 = blk_ld(sl, kX0);
-        XRow<K> E1, L1;
-        if (s1 < S) {
-          E1 = blk_ld(sl, kE1);
-          L1 = blk_ld(sl, kX1);
-        }
         const XRow<K> A0 = (gp == 0) ? row_ld(qc) : lds_xrow<K>(outr + (size_t)(gp % kR2) * Up + pr);
         // beta[s1]: beta[S-1] itself when s1 = S-1 (odd, stored), else one step down from the
         // stored beta[2k+2]; beta[s0] only for the debug rows
@@ -414,39 +428,53 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
         if (s1 < S) Bt = row_ld((s1 == S - 1) ? (S >> 1) : k + 1);
         if (dbg) Bs0 = (s0 == M) ? lds_xrow<K>(cutb + pr) : row_ld(k);
         cbar();
-        ctr_st(&ctl->help[0][h], i + 1);  // ring slot and ring row read (in-order DS): reusable
+        ctr_st(&ctl->help[0][h], i + 1);  // ring row read (in-order DS): reusable
+        if (PEXP(0)) return;
+        XRow<K> E0, Sh0, E1, Sh1;
+        convert<K, false>(r0, P, lane, E0, Sh0);
         if (s1 < S) {
-          const XRow<K> Sh1 = unshift<K>(L1, p0, P);
+          convert<K, false>(r1, P, lane, E1, Sh1);
           XRow<K> B1 = Bt, B2 = Bt;
           if (s1 + 1 < S) beta_chain<K, false, true>(B1, E1, Sh1, ONE);  // beta[s1] from beta[2k+2]
-          emit(s0, A0, E0, unshift<K>(L0, p0, P), B1, Bs0);
+          emit(s0, A0, E0, Sh0, B1, Bs0);
           XRow<K> A1 = A0;  // alpha[s1] = one step from alpha[s0]
-          alpha_chain<K, false, true>(A1, E0, L0, ONE);
+          alpha_chain<K, false, true>(A1, E0, preshift<K>(Sh0), ONE);
           emit(s1, A1, E1, Sh1, B2, B1);  // (s1 = S-1: the terminal row; B2 unused)
         } else {
-          emit(s0, A0, E0, unshift<K>(L0, p0, P), Bt, Bs0);  // s0 = S-1: the terminal row
+          emit(s0, A0, E0, Sh0, Bt, Bs0);  // s0 = S-1: the terminal row
         }
       } else {
-        const int k = qc - 1 - gp;  // lattice pair (2k, 2k+1); beta stream index kmax - k
+        const int k = qc - 1 - gp;  // lattice pair (2k, 2k+1); beta stream entry kmax - k
         const int s0 = 2 * k, s1 = s0 + 1;
         const int j = kmax - k;
-        if (gp > 0) wait_chain(j);                // beta[2k+2]: stream entry j - 1 done
-        if (dbg) wait_chain(j + 1);               // beta[2k]: stream entry j
-        const xf* sl = slot_of(1, j);
-        const XRow<K> E0 = blk_ld(sl, kE0), Sh0 = blk_ld(sl, kX0);
-        const XRow<K> E1 = blk_ld(sl, kE1), Sh1 = blk_ld(sl, kX1);
-        XRow<K> B2 = (gp == 0) ? lds_xrow<K>(cutb + pr) : lds_xrow<K>(outr + (size_t)(kR2 + gp % kR2) * Up + pr);
-        XRow<K> A0 = row_ld(k);
+        if (gp > 0) wait_chain(j);  // beta[2k+2]: stream entry j - 1 done
+        if (dbg) wait_chain(j + 1); // beta[2k]: stream entry j
+        const XRow<K> B2 = (gp == 0) ? lds_xrow<K>(cutb + pr) : lds_xrow<K>(outr + (size_t)(kR2 + gp % kR2) * Up + pr);
+        const XRow<K> A0 = row_ld(k);
         XRow<K> Bs0;
         if (dbg) Bs0 = lds_xrow<K>(outr + (size_t)(kR2 + (gp + 1) % kR2) * Up + pr);
         cbar();
         ctr_st(&ctl->help[1][h], i + 1);
+        if (PEXP(0)) return;
+        XRow<K> E0, Sh0, E1, Sh1;
+        convert<K, false>(r0, P, lane, E0, Sh0);
+        convert<K, false>(r1, P, lane, E1, Sh1);
         XRow<K> B1 = B2;  // beta[s1] = one step down from beta[2k+2]
         beta_chain<K, false, true>(B1, E1, Sh1, ONE);
         XRow<K> A1 = A0;  // alpha[s1] = one step from alpha[2k]
         alpha_chain<K, false, true>(A1, E0, preshift<K>(Sh0), ONE);
         emit(s0, A0, E0, Sh0, B1, Bs0);
         emit(s1, A1, E1, Sh1, B2, B1);
+      }
+    };
+    Item<K, false> a0, a1, b0, b1;  // alternating buffers: pair i+1 loads while pair i computes
+    if (nmine > 0) gload(0, a0, a1);
+    for (int i = 0; i < nmine; i += 2) {
+      if (i + 1 < nmine) gload(i + 1, b0, b1);
+      body(i, a0, a1);
+      if (i + 1 < nmine) {
+        if (i + 2 < nmine) gload(i + 2, a0, a1);
+        body(i + 1, b0, b1);
       }
     }
     dg.flush(b, role.slot);
@@ -460,9 +488,16 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
     constexpr int D = kPairConvDepth;
     const unsigned tag0 = (d == 0 && c == 0 && b == 0 && a.loss_sum) ? sum_tag(a) : 0u;
     const int chain_end = d == 0 ? nA : nstream;  // stream entries the chain reads
-    const int hb = d == 0 ? hbf : hbb;            // first stream entry the gradient waves read
     // stream entry j -> lattice pair k: forward j, backward kmax - j
     auto load = [&](int j, Item<K, false>& r0, Item<K, false>& r1) {
+      if (PEXP(15)) {  // (experiment 15: no loads)
+#pragma unroll
+        for (int q = 0; q < 2 * K; ++q) {
+          r0.lt[q] = -0.5f - 0.01f * j;
+          r1.lt[q] = -0.7f - 0.01f * j;
+        }
+        return;
+      }
       const int k = d == 0 ? j : kmax - j;
       const int row0 = min(max(2 * k, 0), T - 1), row1 = min(max(2 * k + 1, 0), T - 1);
       gld<K, 2, NV>(r0.lt, brsrc(lt + (size_t)row0 * U * 2, U * 8u), p0);
@@ -472,50 +507,82 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
 #pragma unroll
     for (int i = 0; i < D; ++i) load(c + kNC * i, pf0[i], pf1[i]);
     int seen_chain = 0;
-    int seen_grad = 0;  // gradient pairs known done
     const int nmine = (nstream - c + kNC - 1) / kNC;  // my stream entries: c, c + kNC, ...
-    for (int base = 0; base < nmine; base += D) {
+    // Two entries per group, their math interleaved (a converter's instruction stream is
+    // latency-bound at ~5 cycles per dependent VALU; two independent streams fill the gaps), one
+    // loop per direction so the group is branch-free.
+    static_assert(D % 2 == 0, "entries are converted two at a time");
+    auto conv_loop = [&](auto Fwd) {
+      constexpr bool FWD = decltype(Fwd)::value;
+      auto math = [&](int n, const Item<K, false>& r0, const Item<K, false>& r1, XRow<K>* o) {
+        // o: C0 C1 C2 E0 E1 X0
+        const int j = c + kNC * n;
+        const int k = FWD ? j : kmax - j;
+        const int P1 = (2 * k + 1 < S) ? P : 0;  // row 2k+1 beyond S: all factors zero
+        XRow<K> S0, S1;
+        if (PEXP(1)) {
 #pragma unroll
-      for (int i = 0; i < D; ++i) {
-        const int n = base + i;
-        if (n < nmine) {
-          const int j = c + kNC * n;
-          const int k = d == 0 ? j : kmax - j;
-          const int P1 = (2 * k + 1 < S) ? P : 0;  // row 2k+1 beyond S: all factors zero
-          XRow<K> E0, S0, E1, S1;
-          convert<K, false>(pf0[i], P, lane, E0, S0);
-          convert<K, false>(pf1[i], P1, lane, E1, S1);
-          const XRow<K> X0 = d == 0 ? preshift<K>(S0) : S0;
-          const XRow<K> X1 = d == 0 ? preshift<K>(S1) : S1;
-          XRow<K> C0, C1, C2;
-          if (d == 0) pair_coefs<K, true>(E0, X0, E1, X1, C0, C1, C2);
-          else pair_coefs<K, false>(E0, X0, E1, X1, C0, C1, C2);
-          // slot j % R last held entry q = j - R: the chain and the gradient waves must be done
-          const int q = j - R;
-          if (q >= 0) {
-            const int need_c = min(q + 1, chain_end);
-            if (seen_chain < need_c)
-              seen_chain = spin_until<true>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
-            if (q >= hb && seen_grad <= q - hb)
-              seen_grad = spin_until<true>([&] { return first_missing<kNH>(ctl->help[d], 0); }, q - hb + 1, a.status, dg);
+          for (int q = 0; q < K; ++q) {
+            o[3].m[q] = r0.lt[2 * q]; o[3].e[q] = 0; o[5].m[q] = r0.lt[2 * q + 1]; o[5].e[q] = -1;
+            o[4].m[q] = r1.lt[2 * q]; o[4].e[q] = 0;
           }
-          cbar();
-          xf* sl = slot_of(d, j);
-          auto put = [&](int k2, const XRow<K>& r) { lds_xrow_st<K>(act ? sl + (size_t)k2 * blk + p0 : junk_lane, r); };
-          put(kC0, C0);
-          put(kC1, C1);
-          put(kC2, C2);
-          put(kE0, E0);
-          put(kX0, X0);
-          put(kE1, E1);
-          put(kX1, X1);
-          cbar();
-          ctr_st(&ctl->conv[d][c], n + 1);
+          o[0] = o[3]; o[1] = o[5]; o[2] = o[4];
+          return;
         }
-        // refill after the old item is consumed (same registers, no copy)
-        load(c + kNC * (n + D), pf0[i], pf1[i]);
+        convert<K, false>(r0, P, lane, o[3], S0);
+        convert<K, false>(r1, P1, lane, o[4], S1);
+        o[5] = FWD ? preshift<K>(S0) : S0;
+        const XRow<K> X1 = FWD ? preshift<K>(S1) : S1;
+        pair_coefs<K, FWD>(o[3], o[5], o[4], X1, o[0], o[1], o[2]);
+      };
+      auto put_entry = [&](int n, const XRow<K>* o) {
+        const int j = c + kNC * n;
+        xf* sl = slot_of(d, j);
+        auto put = [&](int k2, const XRow<K>& r) {
+          if (!PEXP(14)) lds_xrow_st<K>(act ? sl + (size_t)k2 * blk + p0 : junk_lane, r);  // (14: no ring writes)
+        };
+        if (!FWD && j == 0) {
+          // the backward chain's first entry: E of row S-1 (terminal emit) and, S-1 odd, the
+          // factors of row S-2 for its one ordinary step (this pair's coefficients are unused)
+          const bool odd = ((S - 1) & 1) != 0;
+          put(kC0, odd ? o[4] : o[3]);
+          put(kC1, o[3]);
+          put(kC2, o[5]);
+        } else {
+          put(kC0, o[0]);
+          put(kC1, o[1]);
+          put(kC2, o[2]);
+        }
+      };
+      for (int base = 0; base < nmine; base += D) {
+#pragma unroll
+        for (int i = 0; i < D; i += 2) {
+          const int n0 = base + i, n1 = n0 + 1;
+          if (n0 < nmine) {
+            XRow<K> o0[6], o1[6];
+            math(n0, pf0[i], pf1[i], o0);
+            math(n1, pf0[i + 1], pf1[i + 1], o1);  // (past the end: garbage, never stored)
+            // slots of entries n0, n1 last held entries j - R: the chain must have read them
+            const int q = c + kNC * min(n1, nmine - 1) - R;
+            if (q >= 0 && !PEXP(13)) {
+              const int need_c = min(q + 1, chain_end);
+              if (seen_chain < need_c)
+                seen_chain = spin_until<true>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
+            }
+            cbar();
+            put_entry(n0, o0);
+            if (n1 < nmine) put_entry(n1, o1);
+            cbar();
+            ctr_st(&ctl->conv[d][c], min(n1, nmine - 1) + 1);
+          }
+          // refill after the old items are consumed (same registers, no copy)
+          load(c + kNC * (n0 + D), pf0[i], pf1[i]);
+          load(c + kNC * (n1 + D), pf0[i + 1], pf1[i + 1]);
+        }
       }
-    }
+    };
+    if (d == 0) conv_loop(std::true_type{});
+    else conv_loop(std::false_type{});
     dg.flush(b, role.slot);
     fill_rows(S, d * kNC + c, 2 * kNC);  // zero the rows beyond S
     if (d == 0 && c == 0 && b == 0 && a.loss_sum) finish_loss_sum(a, tag0);
@@ -529,6 +596,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
   const int d = role.d;
   int ready = 0;  // stream entries known converted
   auto wait_entry = [&](int j) {
+    if (PEXP(3)) return;
     if (j >= ready)
       ready = spin_until<false>([&] { return first_missing<kNC>(ctl->conv[d], 0); }, j + 1, a.status, dg);
   };
@@ -544,8 +612,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
     C1b[par] = lds_xrow<K>(cptr[j] + blk);
     C2b[par] = lds_xrow<K>(cptr[j] + 2 * blk);
   };
-  constexpr int H1 = R / 2;                 // sub-block before the cut
-  constexpr int H2 = R / 4 > 2 ? R / 4 : 2; // past the cut (ring rows released right behind)
+  constexpr int H1 = 4;  // sub-block before the cut
+  constexpr int H2 = 2;  // past the cut (chain-ring rows released right behind)
   // steps [lo, hi) of stream entries, blocks of R aligned to R
   auto run = [&](auto Hc, int lo, int hi, auto&& step, auto&& hwait) {
     constexpr int HS = decltype(Hc)::value;
@@ -588,7 +656,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
       wait_entry(min(r1 - 1 + PF, last));
       if (phase2) {  // ring entries for steps up to r1-1: g = step + 1 - qc; previous occupant g - kR2
         const int gq = r1 - qc - kR2;
-        if (gq >= 1 && help_seen <= gq)
+        if (gq >= 1 && help_seen <= gq && !PEXP(11))
           help_seen = spin_until<false>([&] { return first_missing<kNH>(ctl->help[0], 0); }, gq + 1, a.status, dg);
       }
       cbar();
@@ -645,7 +713,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
     cbar();
     {
       const xf* sl = ring0 + (size_t)R * slot;  // backward slot 0
-      const XRow<K> Et = blk_ld(sl, ((S - 1) & 1) ? kE1 : kE0);  // factors of row S-1
+      const XRow<K> Et = blk_ld(sl, kC0);  // E of row S-1 (converter entry 0)
 #pragma unroll
       for (int j = 0; j < K; ++j) {  // beta[S-1]: terminal emit (src/lib.rs:187-195)
         const bool lastp = (p0 + j) == P - 1;
@@ -655,7 +723,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
       }
       put_row(S - 1, X);
       if ((S - 1) & 1) {  // beta[S-2] = one step down with the factors of row S-2
-        const XRow<K> E0 = blk_ld(sl, kE0), Sh0 = blk_ld(sl, kX0);
+        const XRow<K> E0 = blk_ld(sl, kC1), Sh0 = blk_ld(sl, kC2);  // row S-2
         cbar();
         beta_chain<K, false, true>(X, E0, Sh0, X);
         put_row(S - 2, X);
@@ -671,7 +739,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_pair(F
       wait_entry(min(r1 - 1 + PF, nstream - 1));
       if (ring) {  // entries up to r1-1 write ring entries g = j - jcut; previous occupant g - kR2
         const int gq = r1 - 1 - jcut - kR2;
-        if (gq >= 1 && help_seen <= gq)
+        if (gq >= 1 && help_seen <= gq && !PEXP(11))
           help_seen = spin_until<false>([&] { return first_missing<kNH>(ctl->help[1], 0); }, gq + 1, a.status, dg);
       }
       cbar();
@@ -765,8 +833,8 @@ size_t pair_storage_bytes(int K, int T, int U) {
 
 int launch_fwd_bwd_pair(const FwdBwdArgs& a, hipStream_t st) {
   if (a.log_obs || a.grad_obs || a.U > 128) return SSNT_ERR_UNSUPPORTED;
-  if (a.U <= 64) return launch_pair_k<1, 8>(a, st);
-  return pair_slots_for(2 * ((a.U + 1) / 2)) == 8 ? launch_pair_k<2, 8>(a, st) : launch_pair_k<2, 4>(a, st);
+  if (a.U <= 64) return launch_pair_k<1, pair_slots_for(64)>(a, st);
+  return pair_slots_for(2 * ((a.U + 1) / 2)) == 16 ? launch_pair_k<2, 16>(a, st) : launch_pair_k<2, 8>(a, st);
 }
 
 }  // namespace ssnt

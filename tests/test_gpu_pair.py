@@ -1,5 +1,4 @@
-"""GPU parity for the pair kernel (csrc/fwd_bwd_pair.hip): the default fwd-bwd for U <= 128
-without log_obs. Bit-exact against the oracle's pair recurrence (oracle.fwd_bwd_xf(pair=True),
+"""GPU parity for the pair kernel (csrc/fwd_bwd_pair.hip): variant 12, U <= 128 without log_obs. Bit-exact against the oracle's pair recurrence (oracle.fwd_bwd_xf(pair=True),
 ORACLE_PAIR in oracle/ssnt_oracle.c), which tests/test_oracle_fwd_bwd.py pins to the float64
 DP and to brute-force path enumeration within the north_star tolerance.
 
@@ -15,6 +14,16 @@ import torch
 pytestmark = pytest.mark.gpu
 
 F_TERM, F_ZINF = 1, 2
+
+
+@pytest.fixture(autouse=True)
+def pair_variant(gpu):
+    """The pair kernel is selected with ssnt_fwd_bwd_set_variant(12) (the default dispatch keeps
+    the one-step streaming kernel, which measured faster: DESIGN.md 5.1a)."""
+    lib = gpu.load()
+    assert lib.ssnt_fwd_bwd_set_variant(12) == 0
+    yield
+    lib.ssnt_fwd_bwd_set_variant(0)
 
 
 def _run(gpu, lt, S, P, flags=F_TERM, debug=True, shift=0):

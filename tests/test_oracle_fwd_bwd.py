@@ -135,3 +135,66 @@ def test_large_magnitudes_long_form_slice(oracle):
     # long-form statistics (|log alpha| in the thousands): f32 rounding dominates, see tolerance
     lt = oracle.synth_log_trans(1, 600, 120, seed=2)
     _xf_vs_f64(oracle, lt, [600], [120])
+
+
+# ---- the pair recurrence (ORACLE_PAIR; the pair kernel, csrc/fwd_bwd_pair.hip) -----------------
+# Even rows two steps at a time, odd rows one step from the even row beside them, an even cut:
+# another rounding order of the same lattice, so the same f64 pins and tolerances apply.
+def _pair_vs_f64(oracle, lt, S, P, flags=F1):
+    a = oracle.fwd_bwd_xf(lt, S, P, flags=flags, debug=True, pair=True)
+    b = oracle.fwd_bwd_f64(lt, S, P, flags=flags)
+    fin = np.isfinite(b["loss"])
+    assert np.array_equal(np.isfinite(a["loss"]), fin)
+    _close_log(a["loss"][fin], b["loss"][fin])
+    assert np.max(np.abs(a["grad"] - b["grad"])) <= 1e-5
+    _close_log(a["log_alpha"], b["log_alpha"])
+    _close_log(a["log_beta"], b["log_beta"])
+    return a, b
+
+
+@pytest.mark.parametrize("terminal", [True, False])
+@pytest.mark.parametrize("case", range(12))
+def test_pair_oracle_vs_brute_force(oracle, case, terminal):
+    rng = np.random.default_rng(case)
+    T, U = 9, 4
+    S = int(rng.integers(1, T + 1))
+    P = int(rng.integers(1, U + 1))
+    lt = oracle.synth_log_trans(1, T, U, seed=case)
+    flags = F1 if terminal else 0
+    o = oracle.fwd_bwd_xf(lt, [S], [P], flags=flags, pair=True)
+    loss, g, _ = LR.brute_force(lt[0], S, P, None, terminal)
+    if np.isinf(loss):
+        assert np.isinf(o["loss"][0]) and np.all(o["grad"] == 0)
+        return
+    assert abs(o["loss"][0] - loss) < 1e-5
+    assert np.max(np.abs(o["grad"][0] - g)) < 1e-6
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_pair_ragged_every_parity(oracle, seed):
+    rng = np.random.default_rng(seed)
+    B, T, U = 12, 61, 24
+    P = rng.integers(1, U + 1, size=B)
+    S = np.array([rng.integers(max(p, 1), T + 1) for p in P])
+    S[:4] = [1, 2, 3, 4]  # cut at 0, the terminal pair alone, both parities of S - 1
+    P[:4] = [1, 2, 2, 3]
+    lt = oracle.synth_log_trans(B, T, U, seed=seed)
+    _pair_vs_f64(oracle, lt, S, P)
+    _pair_vs_f64(oracle, lt, S, P, flags=0)
+
+
+def test_pair_config2_and_long_slice(oracle):
+    lt = oracle.synth_log_trans(4, 200, 80, seed=0)
+    _pair_vs_f64(oracle, lt, [200, 199, 120, 81], [80, 80, 64, 81])
+    lt = oracle.synth_log_trans(1, 600, 120, seed=2)
+    _pair_vs_f64(oracle, lt, [600], [120])
+
+
+def test_pair_posteriors_and_neg_inf(oracle):
+    lt = oracle.synth_log_trans(2, 80, 30, seed=11)
+    lt[1, 3:6, :, 0] = -np.inf
+    a = oracle.fwd_bwd_xf(lt, [80, 64], [30, 21], pair=True)
+    for b, S in enumerate([80, 64]):
+        occ = -(a["grad"][b, :S - 1].sum(axis=(1, 2)))
+        assert np.max(np.abs(occ - 1.0)) < 1e-5
+    _pair_vs_f64(oracle, lt, [80, 64], [30, 21])
