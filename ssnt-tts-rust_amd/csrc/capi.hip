@@ -603,6 +603,9 @@ int ssnt_fused_decode_select(int mode) { return set_fused_decode_select(mode); }
 
 // A/B of the long-row kernel's lane width (tools, tests); not part of the public header.
 int ssnt_fwd_bwd_wide_lanes(int k) { return set_fwd_bwd_wide_lanes(k); }
+// A/B of the long-row kernel's workgroup split (-1 auto, 0 one workgroup per direction, 1 two
+// whenever a direction has 2+ segments); not part of the public header.
+int ssnt_fwd_bwd_wide_split(int mode) { return set_fwd_bwd_wide_split(mode); }
 // A/B of the streaming kernel's ring depth (16 / 32 slots, rows in the workspace; 0 default);
 // not part of the public header.
 int ssnt_fwd_bwd_stream_ring(int r) { return set_stream_ring(r); }

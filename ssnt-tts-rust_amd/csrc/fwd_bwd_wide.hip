@@ -20,7 +20,24 @@
 //       phase 2: both form Z = sum_p alpha[M][p] beta[M][p] (the oracle's binary tree); the
 //       alpha workgroup continues M..S-1 emitting the gradient rows s >= M (beta[s+1] read
 //       back), the beta workgroup continues M-1..0 emitting rows s < M (alpha[s] read back).
-//     The kernel boundary between them is the only inter-workgroup synchronisation.
+//     The kernel boundary between them is the only inter-workgroup synchronisation...
+//   * ...unless the batch leaves CUs idle (4B <= CUs, configs[4]: 64 utterances): then a
+//     direction's segments are split over TWO workgroups (SPLIT). A wave's step is VALU-issue
+//     bound (convert + recurrence + gradients), and 7 waves on one CU's 4 SIMDs put two on a SIMD;
+//     split, each CU holds at most 4 compute waves. The upstream workgroup (the segments the
+//     recurrence flows out of: the low positions for alpha, the high ones for beta) hands its
+//     boundary values to the downstream one through global memory, one block of kBS steps at a
+//     time, by two proxy waves that carry no arithmetic:
+//       publisher (upstream workgroup): reads the last compute wave's LDS ring, stores the block
+//         write-through (sc1), drains its own stores (vmcnt(0): it has no loads in flight) and
+//         advances a global counter (relaxed agent-scope atomic store);
+//       receiver (downstream workgroup): polls that counter (relaxed agent loads + s_sleep), loads
+//         the block with sc1 loads (no L1 copy can be stale, so no acquire fence) and feeds it
+//         into the first compute wave's LDS ring.
+//     The global ring holds every step of the phase, so the upstream workgroup never waits for
+//     the downstream one; the counters are zeroed by a memset node before phase 1 on every call.
+//     Upstream workgroups have the lower block ids (dispatched first) and sit 2B ids before
+//     their partner, so the pair shares an XCD (and its L2) whenever 2B % 8 == 0.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -35,6 +52,8 @@ namespace {
 // steps per hand-off block = rows in flight per wave (ring indices static). At K = 1, 16 rows of
 // 512 B per wave keep ~2 us of HBM latency covered at a ~0.2 us step (Little's law: 8 rows held
 // the kernel near 3 TB/s); K = 2 has twice the bytes per row and the registers for 8.
+// SPLIT phase 1 at K = 1 keeps 32 rows in flight (at most 2 waves per SIMD leave it the
+// registers; configs[4]: 660 -> 625 us), one workgroup per direction 16 (32 measured slower there).
 // (build-time overrides for tuning studies: SSNT_W_D1 / SSNT_W_D2, phase 1 / 2 at K = 1)
 #ifndef SSNT_W_D1
 #define SSNT_W_D1 16
@@ -42,20 +61,39 @@ namespace {
 #ifndef SSNT_W_D2
 #define SSNT_W_D2 16
 #endif
-template <int K, int PHASE>
-constexpr int block_steps() { return K == 1 ? (PHASE == 1 ? SSNT_W_D1 : SSNT_W_D2) : 8; }
+template <int K, int PHASE, bool SPLIT>
+constexpr int block_steps() {
+  return K == 1 ? (PHASE == 1 ? (SPLIT ? 32 : SSNT_W_D1) : SSNT_W_D2) : 8;
+}
 constexpr int kRB = 64;        // hand-off ring slots (steps) per wave
 constexpr int kMaxNW = 8;      // waves per direction: U <= 512 (K = 1) / 1024 (K = 2)
+constexpr int kProxy = kMaxNW; // ring / counter index of the proxy wave (SPLIT)
 constexpr int kSpinMax = 1 << 22;
 
 struct WideCtl {
-  int prod[kMaxNW];     // steps whose hand-off value wave w has written
-  int cons[kMaxNW];     // steps of its upstream ring wave w has read
-  xf zpart[kMaxNW];     // per-segment sums of alpha[M] * beta[M]
+  int prod[kMaxNW + 1];     // steps whose hand-off value ring w holds (w = kProxy: the receiver's)
+  int cons[kMaxNW + 1];     // steps of its upstream ring wave w has read (kProxy: the publisher)
+  xf zpart[kMaxNW];         // per-segment sums of alpha[M] * beta[M]
   xf z;
-  xf bnd[kMaxNW][kRB];  // hand-off rings
-  xf junk[kMaxNW][64];  // where the lanes that do not publish write (branch-free publication)
+  alignas(16) xf bnd[kMaxNW + 1][kRB];  // hand-off rings
+  xf junk[kMaxNW][64];      // where the lanes that do not publish write (branch-free publication)
 };
+
+// Global side of the SPLIT hand-off, carved from the head of the workspace (wide_layout):
+// ctr[phase][b][dir] counters (the memset block), then gring[b][dir][RL] boundary values.
+struct WideGrid {
+  int NW;     // segments (64K positions each) per direction
+  int NWp;    // segments of the upstream workgroup (SPLIT)
+  int* ctr;
+  xf* gring;
+  int RL;     // ring entries per (utterance, direction): T + 32
+  xf* rows;   // rows base (after the sync block)
+};
+
+__device__ __forceinline__ int gctr_ld(const int* p) {
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
 
 // compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>)
 template <typename F, int... I>
@@ -93,6 +131,21 @@ __device__ __forceinline__ void wait_ge(const int* p, int target, int* status) {
   }
 }
 
+// the same on a global counter written by another workgroup (relaxed agent-scope polls)
+__device__ __forceinline__ int gwait_ge(const int* p, int target, int* status) {
+  int v = gctr_ld(p);
+  for (int n = 0; v < target; ++n) {
+    if (n > kSpinMax) {
+      if (status && (threadIdx.x & 63) == 0) atomicOr(status, kStatusTimeout);
+      return target;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    v = gctr_ld(p);
+  }
+  return v;
+}
+constexpr int kSC1 = 16;  // buffer-op cache policy: sc1 (write-through store / L1-bypassing load)
+
 template <int K>
 struct WItem {    // one row's inputs for this lane's K positions
   float lt[2 * K];  // emit/shift of p0 .. p0+K-1
@@ -110,17 +163,35 @@ struct WRows {    // phase-2 workspace rows for this lane
 // step bodies carry no debug branches: straight-line blocks keep the compiler's memory wait
 // counts exact, and a wait for row r+8's loads does not drain the stores issued since)
 // K: positions per lane; a wave owns 64K consecutive positions.
-template <int K, bool OBS, int PHASE, bool DBG>
-__global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
+// SPLIT: a direction's segments over two workgroups (header); 1-D grid of 4B workgroups, id =
+// part * 2B + 2b + dir, part 0 = upstream. Waves in flow order (alpha: increasing positions,
+// beta: decreasing): local wave w < ncomp computes flow segment f0 + w; wave ncomp is the proxy.
+template <int K, bool OBS, int PHASE, bool DBG, bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a, WideGrid gd) {
   constexpr int kSeg = 64 * K;
-  constexpr int kBS = block_steps<K, PHASE>();
+  constexpr int kBS = block_steps<K, PHASE, SPLIT>();
   static_assert(kRB % kBS == 0, "hand-off blocks must tile the ring");
   constexpr int kDepth = kBS;  // rows in flight per wave
   __shared__ WideCtl ctl;
-  const int b = blockIdx.x;
-  const int dir = blockIdx.y;  // 0 alpha, 1 beta
-  const int NW = blockDim.x >> 6;
+  int b, dir, part;  // dir 0 alpha, 1 beta; part 0 upstream, 1 downstream (SPLIT)
+  if constexpr (SPLIT) {
+    const int id = blockIdx.x;
+    part = id >= 2 * a.B ? 1 : 0;
+    const int r = id - part * 2 * a.B;
+    b = r >> 1;
+    dir = r & 1;
+  } else {
+    b = blockIdx.x;
+    dir = blockIdx.y;
+    part = 0;
+  }
+  const int NW = gd.NW;
+  const int ncomp = SPLIT ? (part == 0 ? gd.NWp : NW - gd.NWp) : NW;  // compute waves here
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool comp = w < ncomp;
+  const bool proxy = SPLIT && w == ncomp;
+  const int f = (SPLIT && part == 1 ? gd.NWp : 0) + (comp ? w : 0);  // flow segment
+  const int seg = dir == 0 ? f : NW - 1 - f;
   const int lane = threadIdx.x & 63;
   const int T = a.T, U = a.U;
   // lengths are wave-uniform: every buffer descriptor built from them must live in SGPRs (a
@@ -135,11 +206,11 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   float* go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
   float* la = (DBG && a.log_alpha) ? a.log_alpha + (size_t)b * TU : nullptr;
   float* lb = (DBG && a.log_beta) ? a.log_beta + (size_t)b * TU : nullptr;
-  xf* rows = reinterpret_cast<xf*>(a.workspace) + (size_t)b * (T + 1) * U;  // row T: beta[M]
-  const int p0 = kSeg * w + K * lane;
+  xf* rows = gd.rows + (size_t)b * (T + 1) * U;  // row T: beta[M]
+  const int p0 = kSeg * seg + K * lane;
   const unsigned rowb = (unsigned)U * 8u, rowf = (unsigned)U * 4u;
 
-  if (threadIdx.x < 2 * kMaxNW) reinterpret_cast<int*>(&ctl)[threadIdx.x] = 0;
+  if (threadIdx.x < 2 * (kMaxNW + 1)) reinterpret_cast<int*>(&ctl)[threadIdx.x] = 0;
   __syncthreads();
 
   // ---- row helpers (8-byte granules: any U, rows only 8-byte aligned). Row indices are
@@ -217,10 +288,10 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   const bool feasible = S >= 1 && P >= 1 && S <= T && P <= U && S >= P;
   if (!feasible) {
     if (PHASE == 2 && dir == 0) {
-      if ((S > T || P > U || S < 0 || P < 0) && a.status && threadIdx.x == 0)
+      if ((S > T || P > U || S < 0 || P < 0) && a.status && part == 0 && threadIdx.x == 0)
         atomicOr(a.status, kStatusBadLength);
-      zero_rows(0, T);
-      if (threadIdx.x == 0) a.loss[b] = inf_loss;
+      if (comp) zero_rows(0, T);
+      if (part == 0 && threadIdx.x == 0) a.loss[b] = inf_loss;
     }
     return;
   }
@@ -266,11 +337,13 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
     }
   };
 
-  // ---- the hand-off pipeline: up = the wave whose boundary value this wave needs
-  const int up = dir == 0 ? w - 1 : w + 1;
-  const int dn = dir == 0 ? w + 1 : w - 1;
-  const bool has_up = up >= 0 && up < NW;
-  const bool has_dn = dn >= 0 && dn < NW;
+  // ---- the hand-off pipeline: up = the ring whose boundary values this wave needs (the
+  // previous wave in flow order, or the receiver's), dn = the wave that reads this wave's ring
+  // (the next one, or the publisher)
+  const int up = w > 0 ? w - 1 : kProxy;
+  const int dn = w + 1 < ncomp ? w + 1 : kProxy;
+  const bool has_up = comp && (w > 0 || (SPLIT && part == 1));
+  const bool has_dn = comp && (w + 1 < ncomp || (SPLIT && part == 0));
   const int pub_lane = dir == 0 ? 63 : 0;
   // n iterations in blocks of kBS; step(i, K, bm, be, pm, pe) with K = i % kBS a compile-time
   // constant (register ring indices), (bm, be) the upstream value of iteration i and (pm, pe)
@@ -285,7 +358,7 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
       if (has_up) wait_ge(&ctl.prod[up], i1, a.status);
       if (has_dn) wait_ge(&ctl.cons[dn], i1 - kRB, a.status);
       wbar();
-      const xf* rd = &ctl.bnd[has_up ? up : w][i0 % kRB];
+      const xf* rd = &ctl.bnd[has_up ? up : 0][i0 % kRB];
 #pragma unroll
       for (int k = 0; k < kBS; ++k) {  // (stale values when there is no upstream: unused)
         const xf v = rd[k];
@@ -306,6 +379,42 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
       wbar();
       if (has_dn) wctr_st(&ctl.prod[w], i1);
       if (has_up) wctr_st(&ctl.cons[w], i1);
+    }
+  };
+
+  // SPLIT proxies (header): n steps of hand-off, kBS values per block, 16 B per lane
+  auto run_proxy = [&](int n) __attribute__((always_inline)) {
+    constexpr int kL = kBS / 2;
+    const __amdgpu_buffer_rsrc_t gr = brsrc(gd.gring + (size_t)(b * 2 + dir) * gd.RL, gd.RL * 8u);
+    int* ctr = gd.ctr + ((PHASE - 1) * a.B + b) * 2 + dir;
+    if (part == 0) {  // publisher: the last compute wave's ring -> global
+      const int src = ncomp - 1;
+      for (int i0 = 0; i0 < n; i0 += kBS) {
+        const int i1 = min(i0 + kBS, n);
+        wait_ge(&ctl.prod[src], i1, a.status);
+        wbar();
+        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (lane < kL) v = *reinterpret_cast<const f32x4*>(&ctl.bnd[src][i0 % kRB + 2 * lane]);
+        wbar();
+        wctr_st(&ctl.cons[kProxy], i1);  // (DS in order: the read above is done first)
+        if (lane < kL) rbuf_st4(v, gr, (i0 + 2 * lane) * 8, 0, kSC1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores only
+        if (lane == 0) __hip_atomic_store(ctr, i1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {  // receiver: global -> the first compute wave's upstream ring
+      int seen = 0;
+      for (int i0 = 0; i0 < n; i0 += kBS) {
+        const int i1 = min(i0 + kBS, n);
+        if (seen < i1) seen = gwait_ge(ctr, i1, a.status);
+        asm volatile("" ::: "memory");  // the payload loads stay behind the poll
+        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (lane < kL) v = rbuf_ld4(gr, (i0 + 2 * lane) * 8, 0, kSC1);
+        wait_ge(&ctl.cons[0], i1 - kRB, a.status);
+        wbar();
+        if (lane < kL) *reinterpret_cast<f32x4*>(&ctl.bnd[kProxy][i0 % kRB + 2 * lane]) = v;
+        wbar();
+        wctr_st(&ctl.prod[kProxy], i1);
+      }
     }
   };
 
@@ -374,8 +483,24 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
     }
   };
 
+  // Dead stores (0-byte descriptor: dropped) that give the prefetch prologue the steady state's
+  // load/store pattern. vmcnt counts loads and stores together, and at the block loop's header
+  // the compiler's wait counts take the minimum over the prologue (loads only) and the back edge
+  // (each step's loads + stores): without these, the first steps of every block waited for loads
+  // issued ~8 rows back instead of kDepth.
+  constexpr int kPad = PHASE == 1 ? K * (DBG ? 2 : 1) : K * (1 + (OBS ? 1 : 0) + (DBG ? 1 : 0));
+  // (distinct offsets: identical stores to one address would be merged away)
+  auto vm_pad = [&](int k) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t r = brsrc(rows, 0u);
+#pragma unroll
+    for (int q = 0; q < kPad; ++q) rbuf_st1(0.0f, r, (k * kPad + q) * 4, 0, 0);
+  };
   WItem<K> ring[kDepth];
   if constexpr (PHASE == 1) {
+    if (!comp) {
+      if (proxy) run_proxy(dir == 0 ? M : S - 1 - M);
+      return;
+    }
     if (dir == 0) {
       // ---------------- alpha[0..M]: rows 0..M of the workspace ----------------
       // alpha[0]: 1 at p = 0 (x obs[0][0]). Selects, not conditional stores: the row must stay
@@ -385,7 +510,7 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
         const xf o = xf_exp(lo[0], true);
         a0 = xf_norm(o.m, o.e);
       }
-      const bool first = w == 0 && lane == 0;
+      const bool first = seg == 0 && lane == 0;
       XRow<K> X;  // alpha row of this lane's K positions
       X.m[0] = first ? a0.m : 0.0f;
       X.e[0] = first ? a0.e : XF_EZERO;
@@ -397,7 +522,10 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
       put_row(0, X);
       if constexpr (DBG) { if (la) put_log(la, 0, X); }
 #pragma unroll
-      for (int k = 0; k < kDepth; ++k) load_item(k, ring[k]);
+      for (int k = 0; k < kDepth; ++k) {
+        load_item(k, ring[k]);
+        vm_pad(k);
+      }
       pipeline(M, [&](int r, auto Kc, float bm, int be, float& pm, int& pe, bool live) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
         XRow<K> E, Sh, O;
@@ -425,7 +553,10 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
       put_row(S - 1 > M ? S - 1 : T, X);
       if constexpr (DBG) { if (lb) put_log(lb, S - 1, X); }
 #pragma unroll
-      for (int k = 0; k < kDepth; ++k) load_item(S - 2 - k, ring[k]);
+      for (int k = 0; k < kDepth; ++k) {
+        load_item(S - 2 - k, ring[k]);
+        vm_pad(k);
+      }
       pipeline(S - 1 - M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe, bool live) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
         const int s = S - 2 - i;
@@ -440,37 +571,51 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
     }
     return;
   } else {
-    // ---------------- phase 2: Z at the cut (both workgroups, the oracle's tree) ----------------
-    float v[2 * K], u[2 * K];
-    ld_row(M, v);
-    ld_row(T, u);
-    float wm[K];
-    int we[K];
+    // ---------------- phase 2: Z at the cut (every workgroup, the oracle's tree) ----------------
+    // segment sums (in-lane levels of the tree, pairs (2i, 2i+1) first, then across lanes), then
+    // across segments; the waves of this workgroup cover all NW segments between them
+    const int nwaves = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
+    for (int sg = w; sg < NW; sg += nwaves) {
+      float v[2 * K], u[2 * K];
+      const int ps = kSeg * sg + K * lane;
+      const __amdgpu_buffer_rsrc_t rm = brsrc(rows + (size_t)M * U, rowb);
+      const __amdgpu_buffer_rsrc_t rt = brsrc(rows + (size_t)T * U, rowb);
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const bool live = p0 + j < P;
-      wm[j] = live ? v[2 * j] * u[2 * j] : 0.0f;
-      we[j] = live ? __builtin_bit_cast(int, v[2 * j + 1]) + __builtin_bit_cast(int, u[2 * j + 1])
-                   : XF_EZERO;
-    }
-    // in-lane levels of the oracle's tree (pairs (2i, 2i+1) first), then across lanes and waves
-#pragma unroll
-    for (int len = K; len > 1; len >>= 1) {
-#pragma unroll
-      for (int q = 0; q < len / 2; ++q) {
-        const xf t2 = xf_add(wm[2 * q], we[2 * q], wm[2 * q + 1], we[2 * q + 1]);
-        wm[q] = t2.m;
-        we[q] = t2.e;
+      for (int j = 0; j < K; ++j) {
+        const f32x2 x = rbuf_ld2(rm, (ps + j) * 8, 0, 0);
+        const f32x2 y = rbuf_ld2(rt, (ps + j) * 8, 0, 0);
+        v[2 * j] = x.x;
+        v[2 * j + 1] = x.y;
+        u[2 * j] = y.x;
+        u[2 * j + 1] = y.y;
       }
-    }
-    xf z{wm[0], we[0]};
+      float wm[K];
+      int we[K];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const float om = __shfl_xor(z.m, off);
-      const int oe = __shfl_xor(z.e, off);
-      z = xf_add(z.m, z.e, om, oe);
+      for (int j = 0; j < K; ++j) {
+        const bool live = ps + j < P;
+        wm[j] = live ? v[2 * j] * u[2 * j] : 0.0f;
+        we[j] = live ? __builtin_bit_cast(int, v[2 * j + 1]) + __builtin_bit_cast(int, u[2 * j + 1])
+                     : XF_EZERO;
+      }
+#pragma unroll
+      for (int len = K; len > 1; len >>= 1) {
+#pragma unroll
+        for (int q = 0; q < len / 2; ++q) {
+          const xf t2 = xf_add(wm[2 * q], we[2 * q], wm[2 * q + 1], we[2 * q + 1]);
+          wm[q] = t2.m;
+          we[q] = t2.e;
+        }
+      }
+      xf z{wm[0], we[0]};
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const float om = __shfl_xor(z.m, off);
+        const int oe = __shfl_xor(z.e, off);
+        z = xf_add(z.m, z.e, om, oe);
+      }
+      if (lane == 0) ctl.zpart[sg] = z;
     }
-    if (lane == 0) ctl.zpart[w] = z;
     __syncthreads();
     if (threadIdx.x == 0) {
       xf t[kMaxNW];
@@ -486,13 +631,15 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
     __syncthreads();
     const xf Z = ctl.z;
     if (Z.m == 0.0f) {  // no path: every output row is the infeasible one
-      if (dir == 0) {
-        zero_rows(0, T);
-        if (threadIdx.x == 0) a.loss[b] = inf_loss;
-      }
+      if (dir == 0 && comp) zero_rows(0, T);
+      if (dir == 0 && part == 0 && threadIdx.x == 0) a.loss[b] = inf_loss;
       return;
     }
-    if (dir == 0 && threadIdx.x == 0) a.loss[b] = 0.0f - xf_log(Z);
+    if (dir == 0 && part == 0 && threadIdx.x == 0) a.loss[b] = 0.0f - xf_log(Z);
+    if (!comp) {
+      if (proxy) run_proxy(dir == 0 ? S - M : M);
+      return;
+    }
     const float izm = 1.0f / Z.m;
     const int ize = -Z.e;
     WRows<K> wr[kDepth];
@@ -510,12 +657,14 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
           r.nob = rbuf_ld1(brsrc(lo + (size_t)uni(min(s + 1, T - 1)) * U, rowf), (p0 + K) * 4, 0, 0);
         }
       };
+      float v[2 * K];
       ld_row(M, v);
       XRow<K> X = unpack(v);
 #pragma unroll
       for (int k = 0; k < kDepth; ++k) {
         load_item(M + k, ring[k]);
         load_rows(M + k, wr[k]);
+        vm_pad(k);
       }
       pipeline(S - M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe, bool live) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
@@ -571,6 +720,7 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
       zero_rows(S, T);  // rows past the lattice
     } else {
       // ---------------- beta: rows M-1..0, gradient rows s < M ----------------
+      float v[2 * K];
       ld_row(T, v);
       XRow<K> X = unpack(v);
       auto load_rows = [&](int s, WRows<K>& r) __attribute__((always_inline)) { ld_row(max(s, 0), r.r0); };  // alpha[s]
@@ -578,6 +728,7 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
       for (int k = 0; k < kDepth; ++k) {
         load_item(M - 1 - k, ring[k]);
         load_rows(M - 1 - k, wr[k]);
+        vm_pad(k);
       }
       pipeline(M, [&](int i, auto Kc, float bm, int be, float& pm, int& pe, bool live) __attribute__((always_inline)) {
         constexpr int k = decltype(Kc)::value;
@@ -608,14 +759,62 @@ __global__ __launch_bounds__(64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a) {
   }
 }
 
+// workspace carve (WideGrid): the counter block first (the memset zeroes exactly it), then the
+// global hand-off rings, then the rows; every piece a multiple of 256 B
+struct WideLayout {
+  size_t ctr, gring, rows;
+};
+inline WideLayout wide_layout(int B, int T, int U) {
+  auto r256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  WideLayout l;
+  l.ctr = r256((size_t)16 * B);  // ctr[2 phases][B][2 dirs]
+  l.gring = r256((size_t)B * 2 * ((size_t)T + 32) * sizeof(xf));
+  l.rows = (size_t)B * ((size_t)T + 1) * U * sizeof(xf);  // rows 0..T-1 + the cut row T
+  return l;
+}
+
+std::atomic<int> g_wide_split{-1};  // -1 auto (4B <= CUs), 0 never, 1 whenever NW >= 2
+
+int device_cus() {
+  static std::atomic<int> cus[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  int n = cus[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cus[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
+}
+
 template <int K, bool OBS, bool DBG>
 int launch_wide(const FwdBwdArgs& a, hipStream_t st) {
   const int NW = (a.U + 64 * K - 1) / (64 * K);
+  const WideLayout l = wide_layout(a.B, a.T, a.U);
+  unsigned char* ws = reinterpret_cast<unsigned char*>(a.workspace);
+  WideGrid gd;
+  gd.NW = NW;
+  gd.NWp = (NW + 1) / 2;
+  gd.ctr = reinterpret_cast<int*>(ws);
+  gd.gring = reinterpret_cast<xf*>(ws + l.ctr);
+  gd.RL = a.T + 32;  // whole blocks of up to 32 steps
+  gd.rows = reinterpret_cast<xf*>(ws + l.ctr + l.gring);
+  const int mode = g_wide_split.load(std::memory_order_relaxed);
+  const bool split = NW >= 2 && (mode == 1 || (mode == -1 && 4 * a.B <= device_cus()));
+  if (split) {
+    if (hipMemsetAsync(gd.ctr, 0, l.ctr, st) != hipSuccess) return SSNT_ERR_HIP;
+    const dim3 grid(4 * a.B), block(64 * (gd.NWp + 1));
+    note_fwd_bwd_dispatch("k_fwd_bwd_wide<K=%d,OBS=%d,DBG=%d,NW=%d,SPLIT>x2", K, (int)OBS, (int)DBG, NW);
+    hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 1, DBG, true>), grid, block, 0, st, a, gd);
+    if (hipGetLastError() != hipSuccess) return SSNT_ERR_HIP;
+    hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 2, DBG, true>), grid, block, 0, st, a, gd);
+    return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
+  }
   const dim3 grid(a.B, 2), block(64 * NW);
   note_fwd_bwd_dispatch("k_fwd_bwd_wide<K=%d,OBS=%d,DBG=%d,NW=%d>x2", K, (int)OBS, (int)DBG, NW);
-  hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 1, DBG>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 1, DBG, false>), grid, block, 0, st, a, gd);
   if (hipGetLastError() != hipSuccess) return SSNT_ERR_HIP;
-  hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 2, DBG>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 2, DBG, false>), grid, block, 0, st, a, gd);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
@@ -631,7 +830,8 @@ std::atomic<int> g_wide_k{1};  // positions per lane (A/B hook ssnt_fwd_bwd_wide
 }  // namespace
 
 size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U) {
-  return (size_t)B * ((size_t)T + 1) * U * sizeof(xf);  // rows 0..T-1 + the cut row T
+  const WideLayout l = wide_layout(B, T, U);
+  return l.ctr + l.gring + l.rows;
 }
 
 int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t st, bool any_u) {
@@ -650,6 +850,12 @@ int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t st, bool any_u) {
 int set_fwd_bwd_wide_lanes(int k) {
   if (k != 1 && k != 2) return SSNT_ERR_INVALID_ARG;
   g_wide_k.store(k);
+  return SSNT_OK;
+}
+
+int set_fwd_bwd_wide_split(int mode) {
+  if (mode < -1 || mode > 1) return SSNT_ERR_INVALID_ARG;
+  g_wide_split.store(mode);
   return SSNT_OK;
 }
 

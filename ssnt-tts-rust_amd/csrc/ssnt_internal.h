@@ -51,6 +51,7 @@ int stream_ring();
 int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t stream, bool any_u);
 size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U);
 int set_fwd_bwd_wide_lanes(int k);  // A/B: positions per lane of the long-row kernel (1 or 2)
+int set_fwd_bwd_wide_split(int mode);  // A/B: two workgroups per direction (-1 auto, 0 off, 1 on)
 size_t stream_head_bytes(int K, int U, bool obs, int ring = 0);  // LDS bytes besides the lattice rows
 // pair kernel (fwd_bwd_pair.hip): U <= 128 without log_obs; SSNT_ERR_UNSUPPORTED otherwise
 int launch_fwd_bwd_pair(const FwdBwdArgs& a, hipStream_t stream);

@@ -126,15 +126,21 @@ def test_config5_long_form_bit_exact(gpu, oracle):
     _assert_bit_exact(g, o, ["loss", "grad"])
 
 
-@pytest.fixture(params=[1, 2], ids=["K1", "K2"])
+@pytest.fixture(params=[(1, 1), (1, 0), (2, 1), (2, 0)], ids=["K1", "K1-one-wg", "K2", "K2-one-wg"])
 def wide_lanes(request, gpu):
-    """The long-row kernel's two lane widths (positions per lane) must be bit-identical."""
+    """The long-row kernel's two lane widths (positions per lane), each with a direction's
+    segments split over two workgroups (global hand-off) and in one workgroup, must be
+    bit-identical."""
     import ctypes
     lib = gpu.load()
     lib.ssnt_fwd_bwd_wide_lanes.restype = ctypes.c_int
-    assert lib.ssnt_fwd_bwd_wide_lanes(request.param) == 0
-    yield request.param
+    lib.ssnt_fwd_bwd_wide_split.restype = ctypes.c_int
+    k, split = request.param
+    assert lib.ssnt_fwd_bwd_wide_lanes(k) == 0
+    assert lib.ssnt_fwd_bwd_wide_split(split) == 0
+    yield k
     lib.ssnt_fwd_bwd_wide_lanes(1)
+    lib.ssnt_fwd_bwd_wide_split(-1)
 
 
 WIDE_SHAPES = [  # the long-row kernel (256 < U <= 512): 3..8 waves per direction, odd U

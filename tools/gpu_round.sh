@@ -6,7 +6,7 @@ TAG=${1:-r2}
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 500 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_${TAG}.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_${TAG}.log; exit 1; }
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu_${TAG}.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_${TAG}.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu_${TAG}.log
 timeout -k 10 300 python3 bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
 cat gpurun_out/bench_${TAG}.json
