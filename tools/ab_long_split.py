@@ -16,9 +16,12 @@ import ssnt_tts_amd as S  # noqa: E402
 from bench_configs import gpu_time  # noqa: E402
 
 B, T, U = (int(x) for x in (sys.argv[1:4] if len(sys.argv) >= 4 else (64, 2000, 400)))
+LANES = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # positions per lane (ssnt_fwd_bwd_wide_lanes)
 dev = torch.device("cuda:0")
 lib = S.load()
 lib.ssnt_fwd_bwd_wide_split.restype = ctypes.c_int
+lib.ssnt_fwd_bwd_wide_lanes.restype = ctypes.c_int
+assert lib.ssnt_fwd_bwd_wide_lanes(LANES) == 0
 g = torch.Generator(device=dev).manual_seed(4)
 lt = torch.log_softmax(torch.randn((B, T, U, 2), device=dev, generator=g) * 1.5, -1).contiguous()
 sl = torch.full((B,), T, dtype=torch.int32, device=dev)
@@ -36,9 +39,10 @@ for mode in (0, 1, 0, 1):
     else:
         res[mode] = (out["loss"].clone(), out["grad"].clone())
         same = True
-    print(json.dumps({"B": B, "T": T, "U": U, "split": mode, "kernel": kern, "us": round(t * 1e6, 1),
+    print(json.dumps({"B": B, "T": T, "U": U, "lanes": LANES, "split": mode, "kernel": kern, "us": round(t * 1e6, 1),
                       "repeat_identical": same}), flush=True)
 lib.ssnt_fwd_bwd_wide_split(-1)
+lib.ssnt_fwd_bwd_wide_lanes(1)
 ident = torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 print(json.dumps({"split_vs_one_workgroup_bit_identical": ident}), flush=True)
 assert ident
