@@ -58,8 +58,6 @@ struct HostCtx {
   unsigned* flag_h = nullptr;  // completion word in coherent pinned memory (host side) ...
   unsigned* flag_d = nullptr;  // ... and its device address
   unsigned seq = 0;            // last completion value requested
-  unsigned* done_ctr = nullptr;  // device counter of finished step workgroups (sync mode 3) ...
-  unsigned done_base = 0;        // ... and its value once every launch so far has finished
 };
 thread_local HostCtx g_ctx;
 
@@ -84,7 +82,6 @@ int ctx_ready(const char* fn, bool abort_on_error) {
     if (g_ctx.d) (void)hipFree(g_ctx.d);
     if (g_ctx.h) (void)hipHostFree(g_ctx.h);
     if (g_ctx.flag_h) (void)hipHostFree(g_ctx.flag_h);
-    if (g_ctx.done_ctr) (void)hipFree(g_ctx.done_ctr);
     g_ctx = HostCtx{};
     g_ctx.device = dev;
     if (hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking) != hipSuccess) {
@@ -102,11 +99,6 @@ int ctx_ready(const char* fn, bool abort_on_error) {
       *g_ctx.flag_h = 0;
     } else if (fh) {
       (void)hipHostFree(fh);
-    }
-    void* dc = nullptr;
-    if (g_ctx.flag_h && hipMalloc(&dc, 256) == hipSuccess) {
-      if (hipMemset(dc, 0, 256) == hipSuccess) g_ctx.done_ctr = static_cast<unsigned*>(dc);
-      else (void)hipFree(dc);
     }
   }
   return SSNT_OK;
@@ -169,11 +161,9 @@ thread_local PhaseClock g_clk;
 // How a per-step call (zero-copy plan) learns that its kernel is done: 0 hipStreamSynchronize;
 // 1 hipStreamWriteValue32 of a sequence number into a coherent pinned word after the kernel,
 // polled by the calling thread; 2 the same word written by a one-thread kernel launched after
-// it; 3 the same word written by the step kernel itself, by its last workgroup to finish (no
-// second launch; decode steps only, the others use 2). A poll that sees nothing for
-// kFlagTimeoutMs falls back to hipStreamSynchronize (which then reports a failed kernel).
-// Default measured per DESIGN.md 7.2 (tools/bench_step_symbols.py).
-std::atomic<int> g_sync_mode{3};
+// it. A poll that sees nothing for kFlagTimeoutMs falls back to hipStreamSynchronize (which
+// then reports a failed kernel). Default measured per DESIGN.md 7.2 (tools/bench_step_symbols.py).
+std::atomic<int> g_sync_mode{2};
 constexpr double kFlagTimeoutMs = 5000.0;
 
 __global__ void k_flag(unsigned* f, unsigned v) {
@@ -182,10 +172,9 @@ __global__ void k_flag(unsigned* f, unsigned v) {
 
 // enqueue the completion write behind the calling thread's kernels and spin until it lands;
 // false: not seen (the caller synchronises)
-bool wait_flag(int mode, bool armed) {
-  const unsigned seq = armed ? g_ctx.seq : ++g_ctx.seq;  // armed: the kernel writes it (arm_done)
-  if (armed) {
-  } else if (mode == 1) {
+bool wait_flag(int mode) {
+  const unsigned seq = ++g_ctx.seq;
+  if (mode == 1) {
     if (hipStreamWriteValue32(g_ctx.stream, g_ctx.flag_d, seq, 0) != hipSuccess) return false;
   } else {
     hipLaunchKernelGGL(k_flag, dim3(1), dim3(1), 0, g_ctx.stream, g_ctx.flag_d, seq);
@@ -222,7 +211,6 @@ struct Plan {
   std::vector<Slot> in, out;
   size_t status_off = 0, total = 0;
   bool zero_copy = false;
-  bool armed = false;  // the kernel writes the completion word itself (sync mode 3)
   char* dbase = nullptr;  // what the kernel addresses: device scratch, or the mapped staging buffer
   static size_t align(size_t x) { return (x + 255) & ~size_t(255); }
   int add_in(const void* src, size_t bytes) {
@@ -291,27 +279,6 @@ int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device =
   return SSNT_OK;
 }
 
-// Sync mode 3: give a step launch the completion word to write (zero-copy plans only).
-void arm_done(Plan& p, StepArgs& a) {
-  if (!p.zero_copy || g_sync_mode.load(std::memory_order_relaxed) != 3 || !g_ctx.flag_h ||
-      !g_ctx.done_ctr || a.B <= 0)
-    return;
-  a.done_flag = g_ctx.flag_d;
-  a.done_ctr = g_ctx.done_ctr;
-  a.done_seq = ++g_ctx.seq;
-  a.done_target = g_ctx.done_base + (unsigned)a.B;
-  p.armed = true;
-}
-// the launch of an armed step: the counter advances only if the kernel was enqueued
-int launch_armed(Plan& p, const StepArgs& a) {
-  const int rc = launch_decode_step(a, g_ctx.stream);
-  if (p.armed) {
-    if (rc == SSNT_OK) g_ctx.done_base = a.done_target;
-    else p.armed = false;
-  }
-  return rc;
-}
-
 // Download status + outputs (one D2H copy, none in zero-copy mode), synchronise, scatter to the
 // caller's arrays. Returns status code.
 int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
@@ -326,8 +293,7 @@ int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
     e = hipMemcpyAsync(g_ctx.h + lo, g_ctx.d + lo, hi - lo, hipMemcpyDeviceToHost, g_ctx.stream);
   }
   const int sync_mode = g_sync_mode.load(std::memory_order_relaxed);
-  if (e == hipSuccess && p.zero_copy && sync_mode != 0 && g_ctx.flag_h &&
-      wait_flag(sync_mode == 3 ? 2 : sync_mode, p.armed))
+  if (e == hipSuccess && p.zero_copy && sync_mode != 0 && g_ctx.flag_h && wait_flag(sync_mode))
     ;  // completion seen through the flag word: the outputs are in the staging buffer
   else if (e == hipSuccess)
     e = hipStreamSynchronize(g_ctx.stream);
@@ -422,8 +388,7 @@ void ssnt_tts_beam_search_decode(const float* h, const float* log_prob_history,
   a.prediction = p.dout<int>(op); a.log_prob = p.dout<float>(ol); a.next_t = p.dout<int>(ot);
   a.next_u = p.dout<int>(ou); a.next_fin = p.dout<bool>(of); a.beam_branch = p.dout<int>(ob);
   a.status = p.dstatus();
-  arm_done(p, a);
-  stage_out(p, launch_armed(p, a), fn, true);
+  stage_out(p, launch_decode_step(a, g_ctx.stream), fn, true);
 }
 
 void ssnt_extract_best_beam_branch(int best_final_branch, const int* beam_branch,
@@ -496,8 +461,7 @@ void ssnt_tts_v2_beam_search_decode(const float* h, const float* log_prob_histor
   a.next_u = p.dout<int>(ou); a.next_fin = p.dout<bool>(of); a.next_total = p.dout<int>(otd);
   a.beam_branch = p.dout<int>(ob);
   a.status = p.dstatus();
-  arm_done(p, a);
-  stage_out(p, launch_armed(p, a), fn, true);
+  stage_out(p, launch_decode_step(a, g_ctx.stream), fn, true);
 }
 
 void ssnt_order_beam_branch(const int* final_branch, const int* beam_branch, int batch_size,
@@ -577,8 +541,7 @@ void tone_latent_beam_search_decode(const float* h, const float* log_prob_histor
   a.prediction = p.dout<int>(op); a.log_prob = p.dout<float>(ol); a.next_t = p.dout<int>(ot);
   a.next_u = p.dout<int>(ou); a.next_fin = p.dout<bool>(of); a.beam_branch = p.dout<int>(ob);
   a.status = p.dstatus();
-  arm_done(p, a);
-  stage_out(p, launch_armed(p, a), fn, true);
+  stage_out(p, launch_decode_step(a, g_ctx.stream), fn, true);
 }
 
 void tone_latent_levenshtein_edit_distance(const int* a, const int* b, const int* a_lengths,
@@ -630,7 +593,7 @@ int ssnt_set_host_staging(int mode) {
 // A/B of how the per-step reference symbols wait for their kernel (g_sync_mode); not part of
 // the public header. Returns the previous mode.
 int ssnt_set_host_sync(int mode) {
-  if (mode < 0 || mode > 3) return -1;
+  if (mode < 0 || mode > 2) return -1;
   return g_sync_mode.exchange(mode);
 }
 

@@ -45,14 +45,6 @@ __global__ __launch_bounds__(64) void k_decode_step(StepArgs a) {
     if (a.next_total) a.next_total[o + i] = r.tot;
   });
   if (nk == 0 && a.status && (threadIdx.x & 63) == 0) atomicOr(a.status, kStatusNoCandidate);
-  if (a.done_flag) {  // the host polls this word instead of synchronising (capi.hip sync mode 3)
-    __threadfence_system();  // this workgroup's outputs and status bits, visible to the host
-    if (threadIdx.x == 0) {
-      const unsigned old = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (old + 1u == a.done_target)
-        __hip_atomic_store(a.done_flag, a.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
 }
 
 // Backtrace along beam_branch (B,T,W) for n_paths (<= 64) final branches per batch element

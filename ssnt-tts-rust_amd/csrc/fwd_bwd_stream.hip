@@ -571,9 +571,6 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // step before the cut also takes ~300 cycles). All LDS
   // addresses are per-lane pointers prepared before the loop (lanes past U: junk / clamped).
   if (!EXP(9)) __builtin_amdgcn_s_setprio(3);  // experiment 9: chains at default priority
-#ifdef SSNT_T_MASKCHAIN
-  if (!act) return;  // tuning study: lanes past U leave the chain (no junk LDS traffic)
-#endif
   const int d = role.d;
   int ready = 0;  // stream rows known converted
   auto wait_row = [&](int r) {  // r: a row that exists

@@ -21,10 +21,9 @@
 //       alpha workgroup continues M..S-1 emitting the gradient rows s >= M (beta[s+1] read
 //       back), the beta workgroup continues M-1..0 emitting rows s < M (alpha[s] read back).
 //     The kernel boundary between them is the only inter-workgroup synchronisation...
-//   * ...unless the batch leaves CUs idle (4B <= CUs, configs[4]: 64 utterances): then a
-//     direction's segments are split over TWO workgroups (SPLIT). A wave's step is VALU-issue
-//     bound (convert + recurrence + gradients), and 7 waves on one CU's 4 SIMDs put two on a SIMD;
-//     split, each CU holds at most 4 compute waves. The upstream workgroup (the segments the
+//   * ...except in the SPLIT form (A/B hook ssnt_fwd_bwd_wide_split; measured slower than the
+//     default): a direction's segments over TWO workgroups, so 64 utterances fill
+//     256 CUs and 7 waves no longer share 4 SIMDs two by two. The upstream workgroup (the segments the
 //     recurrence flows out of: the low positions for alpha, the high ones for beta) hands its
 //     boundary values to the downstream one through global memory, one block of kBS steps at a
 //     time, by two proxy waves that carry no arithmetic:
@@ -213,25 +212,42 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
   if (threadIdx.x < 2 * (kMaxNW + 1)) reinterpret_cast<int*>(&ctl)[threadIdx.x] = 0;
   __syncthreads();
 
-  // ---- row helpers (8-byte granules: any U, rows only 8-byte aligned). Row indices are
-  // wave-uniform; readfirstlane says so to the compiler, so the descriptors stay in SGPRs.
+  // ---- row helpers (8-byte granules: any U, rows only 8-byte aligned). One buffer descriptor
+  // per tensor of this utterance, built once; a row is its scalar offset s * U * 8 (soffset, one
+  // s_mul per access -- per-row descriptors cost ~10 SALU of 64-bit address arithmetic each, a
+  // quarter of a step's instructions). Row indices are wave-uniform (readfirstlane), so the
+  // offsets stay in SGPRs. A lane's position offsets are fixed per lane: positions past U get an
+  // offset beyond every descriptor (loads return 0, stores are dropped: what a row-sized
+  // descriptor did), and the host keeps every descriptor below 2 GB (launch_fwd_bwd_wide).
   auto uni = [](int x) __attribute__((always_inline)) { return __builtin_amdgcn_readfirstlane(x); };
-  auto st_pair = [&](float* base, unsigned bytes, int off, float x0, float x1) __attribute__((always_inline)) {
-    rbuf_st2(f32x2{x0, x1}, brsrc(base, bytes), off, 0, 0);
-  };
+  constexpr int kOOR = (int)0x80000000u;
+  int vo8[K], vo4[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    vo8[j] = p0 + j < U ? (p0 + j) * 8 : kOOR;
+    vo4[j] = p0 + j < U ? (p0 + j) * 4 : kOOR;
+  }
+  const int vnb8 = p0 + K < U ? (p0 + K) * 8 : kOOR;  // the next lane slice's first position
+  const int vnb4 = p0 + K < U ? (p0 + K) * 4 : kOOR;
+  const unsigned tub8 = (unsigned)((size_t)T * U * 8), tub4 = (unsigned)((size_t)T * U * 4);
+  const unsigned wsb8 = (unsigned)((size_t)(T + 1) * U * 8);
+  auto so8 = [&](int s) __attribute__((always_inline)) { return (int)((unsigned)uni(s) * rowb); };
+  auto so4 = [&](int s) __attribute__((always_inline)) { return (int)((unsigned)uni(s) * rowf); };
   // Stores take a `live` flag: a dead step (past the end of the last, partial block) runs the
   // same straight-line code but its descriptors cover 0 bytes, so its stores are dropped.
   auto put_grad = [&](int s, const float* ge, const float* gs, bool live = true) __attribute__((always_inline)) {
     if (!g) return;
-    float* row = g + (size_t)uni(s) * U * 2;
+    const __amdgpu_buffer_rsrc_t r = brsrc(g, live ? tub8 : 0u);
+    const int so = so8(s);
 #pragma unroll
-    for (int j = 0; j < K; ++j) st_pair(row, live ? rowb : 0u, (p0 + j) * 8, ge[j], gs[j]);
+    for (int j = 0; j < K; ++j) rbuf_st2(f32x2{ge[j], gs[j]}, r, vo8[j], so, 0);
   };
   auto put_f = [&](float* base, int s, const float* v, bool live = true) __attribute__((always_inline)) {
     const bool on = live && base != nullptr;  // a null base (output not requested): 0 bytes
-    const __amdgpu_buffer_rsrc_t r = brsrc(on ? base + (size_t)uni(s) * U : nullptr, on ? rowf : 0u);
+    const __amdgpu_buffer_rsrc_t r = brsrc(on ? base : nullptr, on ? tub4 : 0u);
+    const int so = so4(s);
 #pragma unroll
-    for (int j = 0; j < K; ++j) rbuf_st1(v[j], r, (p0 + j) * 4, 0, 0);
+    for (int j = 0; j < K; ++j) rbuf_st1(v[j], r, vo4[j], so, 0);
   };
   auto put_log = [&](float* base, int s, const XRow<K>& x, bool live = true) __attribute__((always_inline)) {
     float v[K];
@@ -242,20 +258,22 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
   // workspace row s (s == T: the cut row). The fields go through registers one by one: a vector
   // built straight from the adjacent fields of the row makes the compiler keep the row in memory
   auto put_row = [&](int s, const XRow<K>& x, bool live = true) __attribute__((always_inline)) {
-    const __amdgpu_buffer_rsrc_t r = brsrc(rows + (size_t)uni(s) * U, live ? rowb : 0u);
+    const __amdgpu_buffer_rsrc_t r = brsrc(rows, live ? wsb8 : 0u);
+    const int so = so8(s);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       float mj = x.m[j];
       int ej = x.e[j];
       asm volatile("" : "+v"(mj), "+v"(ej));
-      rbuf_st2(f32x2{mj, __builtin_bit_cast(float, ej)}, r, (p0 + j) * 8, 0, 0);
+      rbuf_st2(f32x2{mj, __builtin_bit_cast(float, ej)}, r, vo8[j], so, 0);
     }
   };
+  const __amdgpu_buffer_rsrc_t rows_r = brsrc(rows, wsb8);
   auto ld_row = [&](int s, float* v) __attribute__((always_inline)) {  // 2K floats; past U: zeros
-    const __amdgpu_buffer_rsrc_t r = brsrc(rows + (size_t)uni(s) * U, rowb);
+    const int so = so8(s);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const f32x2 x = rbuf_ld2(r, (p0 + j) * 8, 0, 0);
+      const f32x2 x = rbuf_ld2(rows_r, vo8[j], so, 0);
       v[2 * j] = x.x;
       v[2 * j + 1] = x.y;
     }
@@ -297,19 +315,21 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
   }
   const int M = (S - 1) >> 1;
 
+  const __amdgpu_buffer_rsrc_t lt_r = brsrc(lt, tub8);
+  const __amdgpu_buffer_rsrc_t lo_r = brsrc(lo, OBS ? tub4 : 0u);
   auto load_item = [&](int row, WItem<K>& it) __attribute__((always_inline)) {
     row = uni(min(max(row, 0), T - 1));
-    const __amdgpu_buffer_rsrc_t r = brsrc(lt + (size_t)row * U * 2, rowb);
+    const int so = so8(row);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const f32x2 x = rbuf_ld2(r, (p0 + j) * 8, 0, 0);
+      const f32x2 x = rbuf_ld2(lt_r, vo8[j], so, 0);
       it.lt[2 * j] = x.x;
       it.lt[2 * j + 1] = x.y;
     }
     if constexpr (OBS) {
-      const __amdgpu_buffer_rsrc_t o = brsrc(lo + (size_t)uni(min(row + 1, T - 1)) * U, rowf);
+      const int oso = so4(min(row + 1, T - 1));
 #pragma unroll
-      for (int j = 0; j < K; ++j) it.ob[j] = rbuf_ld1(o, (p0 + j) * 4, 0, 0);
+      for (int j = 0; j < K; ++j) it.ob[j] = rbuf_ld1(lo_r, vo4[j], oso, 0);
     }
   };
   auto convert2 = [&](const WItem<K>& it, XRow<K>& E, XRow<K>& Sh, XRow<K>& O) __attribute__((always_inline)) {
@@ -578,12 +598,11 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
     for (int sg = w; sg < NW; sg += nwaves) {
       float v[2 * K], u[2 * K];
       const int ps = kSeg * sg + K * lane;
-      const __amdgpu_buffer_rsrc_t rm = brsrc(rows + (size_t)M * U, rowb);
-      const __amdgpu_buffer_rsrc_t rt = brsrc(rows + (size_t)T * U, rowb);
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const f32x2 x = rbuf_ld2(rm, (ps + j) * 8, 0, 0);
-        const f32x2 y = rbuf_ld2(rt, (ps + j) * 8, 0, 0);
+        const int vo = ps + j < U ? (ps + j) * 8 : kOOR;
+        const f32x2 x = rbuf_ld2(rows_r, vo, so8(M), 0);
+        const f32x2 y = rbuf_ld2(rows_r, vo, so8(T), 0);
         v[2 * j] = x.x;
         v[2 * j + 1] = x.y;
         u[2 * j] = y.x;
@@ -648,13 +667,12 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
       auto load_rows = [&](int s, WRows<K>& r) __attribute__((always_inline)) {  // beta[s+1] (+ position p0+K), beta[s]
         const int sn = uni(min(s + 1, S - 1));
         ld_row(sn, r.r0);
-        const __amdgpu_buffer_rsrc_t rr = brsrc(rows + (size_t)sn * U, rowb);
-        const f32x2 x = rbuf_ld2(rr, (p0 + K) * 8, 0, 0);
+        const f32x2 x = rbuf_ld2(rows_r, vnb8, so8(sn), 0);
         r.nb[0] = x.x;
         r.nb[1] = x.y;
         if constexpr (OBS) {
           ld_row(s == M ? T : min(s, S - 1), r.r1);
-          r.nob = rbuf_ld1(brsrc(lo + (size_t)uni(min(s + 1, T - 1)) * U, rowf), (p0 + K) * 4, 0, 0);
+          r.nob = rbuf_ld1(lo_r, vnb4, so4(min(s + 1, T - 1)), 0);
         }
       };
       float v[2 * K];
@@ -773,7 +791,9 @@ inline WideLayout wide_layout(int B, int T, int U) {
   return l;
 }
 
-std::atomic<int> g_wide_split{-1};  // -1 auto (4B <= CUs), 0 never, 1 whenever NW >= 2
+// -1 auto (4B <= CUs), 0 never (default: with per-utterance descriptors the one-workgroup form
+// is faster, 603 vs 637 us at configs[4]), 1 whenever NW >= 2
+std::atomic<int> g_wide_split{0};
 
 int device_cus() {
   static std::atomic<int> cus[64];
@@ -843,6 +863,8 @@ int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t st, bool any_u) {
     return SSNT_ERR_UNSUPPORTED;
   if (!a.workspace || a.workspace_bytes < fwd_bwd_wide_workspace_bytes(a.B, a.T, a.U))
     return SSNT_ERR_WORKSPACE;
+  // one descriptor per utterance tensor, position offsets up to 2^31 (row helpers)
+  if ((size_t)(a.T + 1) * a.U * 8 >= ((size_t)1 << 31)) return SSNT_ERR_UNSUPPORTED;
   const bool k1 = g_wide_k.load(std::memory_order_relaxed) == 1 && a.U <= 64 * kMaxNW;
   return k1 ? launch_wide_k<1>(a, st) : launch_wide_k<2>(a, st);
 }

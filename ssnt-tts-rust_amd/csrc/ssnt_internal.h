@@ -113,12 +113,6 @@ struct StepArgs {
   int* next_total;  // v2
   int* beam_branch;
   int* status;
-  // completion word (per-step host symbols, sync mode 3; null = off): after its outputs are
-  // visible system-wide, each workgroup adds 1 to *done_ctr; the one that brings it to
-  // done_target writes done_seq to *done_flag (coherent pinned host memory)
-  unsigned* done_flag;
-  unsigned* done_ctr;
-  unsigned done_target, done_seq;
 };
 int launch_decode_step(const StepArgs& a, hipStream_t stream);
 

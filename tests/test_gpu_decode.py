@@ -37,11 +37,11 @@ def select_mode(request, gpu):
     lib.ssnt_fused_decode_select(-1)
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["sync", "writevalue", "flagkernel", "stepflag"])
+@pytest.fixture(params=[0, 1, 2], ids=["sync", "writevalue", "flagkernel"])
 def host_sync(request, gpu):
-    """The per-step host symbols' four ways of waiting for their kernel (hipStreamSynchronize,
-    a hipStreamWriteValue32 completion word, a completion word written by a flag kernel, by the
-    step kernel's last workgroup) must return identical outputs."""
+    """The per-step host symbols' three ways of waiting for their kernel (hipStreamSynchronize,
+    a hipStreamWriteValue32 completion word, a completion word written by a flag kernel) must
+    return identical outputs."""
     import ctypes
     lib = gpu.load()
     lib.ssnt_set_host_sync.restype = ctypes.c_int

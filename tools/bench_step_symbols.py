@@ -109,7 +109,7 @@ def main():
     lib.ssnt_set_host_sync.restype = ctypes.c_int
     lib.ssnt_set_host_sync.argtypes = [ctypes.c_int]
     prev = lib.ssnt_set_host_sync(0)
-    for mode in (0, 1, 2, 3):  # completion: hipStreamSynchronize / hipStreamWriteValue32 / flag kernel / step kernel
+    for mode in (0, 1, 2):  # completion: hipStreamSynchronize / hipStreamWriteValue32 / flag kernel
         lib.ssnt_set_host_sync(mode)
         r = raw_v1(lib, c, n=3000)
         res[f"sync{mode}_raw_gpu_v1_W4_us"] = r["raw_gpu_v1_W4_us"]
