@@ -153,6 +153,51 @@ __device__ __forceinline__ xf f4_butterfly(xf acc) {
   return acc;
 }
 
+// value of the lane at xor distance D (whole wave active): DPP quad permutes for 1 and 2, a
+// ds_swizzle xor for 4..16, a bpermute for 32
+template <int D>
+__device__ __forceinline__ xf xor_xf(xf v) {
+  if constexpr (D == 1) {
+    return dpp_xf<0xB1>(v);
+  } else if constexpr (D == 2) {
+    return dpp_xf<0x4E>(v);
+  } else if constexpr (D < 32) {
+    return xf{__builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v.m), (D << 10) | 0x1F)),
+              __builtin_amdgcn_ds_swizzle(v.e, (D << 10) | 0x1F)};
+  } else {
+    return xf{__shfl_xor(v.m, 32), __shfl_xor(v.e, 32)};
+  }
+}
+
+// The xor butterfly of N classes' 64 lane partials at once, transposed: at distance 1, 2, ...,
+// N/2 a lane keeps half of the classes it still holds (the lower half if its distance bit is 0)
+// and adds its partner's partial of each, so N classes cost N/2 + N/4 + ... + 1 adds instead of
+// N per level; past N/2 each lane holds one class and the plain butterfly finishes it. Every
+// sum is the oracle's f4_butterfly tree node for that class (xf_add is commutative), so the
+// result is bit-identical. Returns the class index (0..N-1) this lane's acc[0] holds; lanes
+// 0..N-1 hold distinct classes.
+template <int N, int Dist = 1>
+__device__ __forceinline__ int f4_reduce_classes(xf (&acc)[N], int lane, int cls = 0) {
+  if constexpr (Dist >= 64) {
+    return cls;
+  } else {
+    constexpr int n = N / Dist;  // classes still in hand (1 once Dist >= N)
+    if constexpr (n > 1) {
+      const bool up = (lane & Dist) != 0;
+#pragma unroll
+      for (int i = 0; i < n / 2; ++i) {
+        const xf keep = up ? acc[n / 2 + i] : acc[i];
+        const xf give = up ? acc[i] : acc[n / 2 + i];
+        acc[i] = f4_add(keep, xor_xf<Dist>(give));
+      }
+      cls += up ? n / 2 : 0;
+    } else {
+      acc[0] = f4_add(acc[0], xor_xf<Dist>(acc[0]));
+    }
+    return f4_reduce_classes<N, Dist * 2>(acc, lane, cls);
+  }
+}
+
 // per-utterance state both kernels derive the same way; false: no lattice (loss written by
 // the forward sweep, every output row zero / -inf)
 __device__ __forceinline__ bool f4_setup(const V2FwdBwdArgs& a, int b, const int* dur, F4Utt& u,
@@ -358,13 +403,6 @@ __global__ __launch_bounds__(kF4GradThreads) void k_f4_grad(V2FwdBwdArgs a) {
   const int ize = -Z.e;
   const unsigned span = hi >= lo ? (unsigned)(hi - lo) : 0u;
   if (hi < lo) lo = 1 << 29;  // empty alpha window: every offset out of range
-  auto emit = [&](int i, xf acc) {
-    const xf S = f4_butterfly(acc);
-    if (lane == 0) {
-      const xf w = xf_exp(a.logits[((size_t)b * Imax + t) * D + i], a.allow_skip || i != a.zid);
-      g[i] = xf_neg_post((S.m * w.m) * izm, S.e + w.e + ize);
-    }
-  };
   constexpr int NCW = (DC + kF4GradWaves - 1) / kF4GradWaves;  // classes per wave
   xf acc[NCW];
   int di[NCW];
@@ -385,9 +423,13 @@ __global__ __launch_bounds__(kF4GradThreads) void k_f4_grad(V2FwdBwdArgs a) {
       acc[j] = xf_add(acc[j].m, acc[j].e, av.m * bv.m, av.e + bv.e);
     }
   }
-#pragma unroll
-  for (int j = 0; j < NCW; ++j)
-    if (wave + j * kF4GradWaves < D) emit(wave + j * kF4GradWaves, acc[j]);  // wave-uniform
+  // every class of this wave reduced at once; lane l < NCW then holds class cls (distinct)
+  const int cls = f4_reduce_classes<NCW>(acc, lane);
+  const int i = wave + cls * kF4GradWaves;
+  if (lane < NCW && i < D) {
+    const xf w = xf_exp(a.logits[((size_t)b * Imax + t) * D + i], a.allow_skip || i != a.zid);
+    g[i] = xf_neg_post((acc[0].m * w.m) * izm, acc[0].e + w.e + ize);
+  }
 }
 
 }  // namespace
