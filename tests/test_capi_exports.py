@@ -76,3 +76,25 @@ def test_mirror_fails_loudly_without_gpu():
     import ssnt_tts_amd as S
     with pytest.raises(RuntimeError):
         S.ssnt_fwd_bwd(torch.zeros(1, 2, 2, 2), torch.ones(1), torch.ones(1))
+
+
+def test_segmented_workspace_query_covers_the_handoff_block():
+    # host-only queries (no HIP call): the long-row kernel's workspace = the hand-off counter
+    # block + the global hand-off rings + its rows (fwd_bwd_wide.hip wide_layout), each piece
+    # padded to 256 B; the A/B hook for its workgroup split takes -1 / 0 / 1 only
+    import ctypes
+    from ssnt_tts_amd._lib import load
+    lib = load()
+    lib.ssnt_fwd_bwd_workspace_size.restype = ctypes.c_size_t
+    lib.ssnt_fwd_bwd_workspace_size.argtypes = [ctypes.c_int] * 3
+    r256 = lambda x: (x + 255) & ~255  # noqa: E731
+    for B, T, U in [(64, 2000, 400), (2, 1030, 1024), (3, 33, 300), (1, 1, 257)]:
+        wide = r256(16 * B) + r256(B * 2 * (T + 32) * 8) + B * (T + 1) * U * 8
+        stream = B * T * (U + 3) * 8
+        assert lib.ssnt_fwd_bwd_workspace_size(B, T, U) == max(wide, stream), (B, T, U)
+    lib.ssnt_fwd_bwd_wide_split.restype = ctypes.c_int
+    lib.ssnt_fwd_bwd_wide_split.argtypes = [ctypes.c_int]
+    for bad in (-2, 2, 7):
+        assert lib.ssnt_fwd_bwd_wide_split(bad) != 0
+    for ok in (-1, 1, 0):
+        assert lib.ssnt_fwd_bwd_wide_split(ok) == 0
