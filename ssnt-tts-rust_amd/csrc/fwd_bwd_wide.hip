@@ -21,9 +21,9 @@
 //       alpha workgroup continues M..S-1 emitting the gradient rows s >= M (beta[s+1] read
 //       back), the beta workgroup continues M-1..0 emitting rows s < M (alpha[s] read back).
 //     The kernel boundary between them is the only inter-workgroup synchronisation...
-//   * ...except in the SPLIT form (A/B hook ssnt_fwd_bwd_wide_split; measured slower than the
-//     default): a direction's segments over TWO workgroups, so 64 utterances fill
-//     256 CUs and 7 waves no longer share 4 SIMDs two by two. The upstream workgroup (the segments the
+//   * ...except in the SPLIT form (small batches, 8B <= CUs, and the 8-wave K = 2 rows; the
+//     rule and its measurements: launch_wide): a direction's segments over TWO
+//     workgroups, so twice the CUs work. The upstream workgroup (the segments the
 //     recurrence flows out of: the low positions for alpha, the high ones for beta) hands its
 //     boundary values to the downstream one through global memory, one block of kBS steps at a
 //     time, by two proxy waves that carry no arithmetic:
@@ -791,9 +791,11 @@ inline WideLayout wide_layout(int B, int T, int U) {
   return l;
 }
 
-// -1 auto (4B <= CUs), 0 never (default: with per-utterance descriptors the one-workgroup form
-// is faster, 603 vs 637 us at configs[4]), 1 whenever NW >= 2
-std::atomic<int> g_wide_split{0};
+// -1 auto (default): split when the unsplit grid would leave most CUs idle (8B <= CUs) or for
+// the heaviest workgroups (K = 2, 8 waves) when 4B <= CUs -- measured per shape, DESIGN.md 5.2
+// (configs[4], B=64 U=400: one workgroup 604 vs split 637 us; B=32: 565 vs 511; B=64 U=1024:
+// 868 vs 749); 0 never; 1 whenever NW >= 2
+std::atomic<int> g_wide_split{-1};
 
 int device_cus() {
   static std::atomic<int> cus[64];
@@ -820,7 +822,13 @@ int launch_wide(const FwdBwdArgs& a, hipStream_t st) {
   gd.RL = a.T + 32;  // whole blocks of up to 32 steps
   gd.rows = reinterpret_cast<xf*>(ws + l.ctr + l.gring);
   const int mode = g_wide_split.load(std::memory_order_relaxed);
-  const bool split = NW >= 2 && (mode == 1 || (mode == -1 && 4 * a.B <= device_cus()));
+  bool split = false;
+  if (NW >= 2 && mode == 1) {
+    split = true;
+  } else if (NW >= 2 && mode == -1) {
+    const int cus = device_cus();
+    split = 8 * a.B <= cus || (K == 2 && NW == kMaxNW && 4 * a.B <= cus);
+  }
   if (split) {
     if (hipMemsetAsync(gd.ctr, 0, l.ctr, st) != hipSuccess) return SSNT_ERR_HIP;
     const dim3 grid(4 * a.B), block(64 * (gd.NWp + 1));

@@ -96,5 +96,5 @@ def test_segmented_workspace_query_covers_the_handoff_block():
     lib.ssnt_fwd_bwd_wide_split.argtypes = [ctypes.c_int]
     for bad in (-2, 2, 7):
         assert lib.ssnt_fwd_bwd_wide_split(bad) != 0
-    for ok in (-1, 1, 0):
+    for ok in (0, 1, -1):
         assert lib.ssnt_fwd_bwd_wide_split(ok) == 0

@@ -140,7 +140,7 @@ def wide_lanes(request, gpu):
     assert lib.ssnt_fwd_bwd_wide_split(split) == 0
     yield k
     lib.ssnt_fwd_bwd_wide_lanes(1)
-    lib.ssnt_fwd_bwd_wide_split(0)
+    lib.ssnt_fwd_bwd_wide_split(-1)
 
 
 WIDE_SHAPES = [  # the long-row kernel (256 < U <= 512): 3..8 waves per direction, odd U

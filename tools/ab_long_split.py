@@ -41,7 +41,7 @@ for mode in (0, 1, 0, 1):
         same = True
     print(json.dumps({"B": B, "T": T, "U": U, "lanes": LANES, "split": mode, "kernel": kern, "us": round(t * 1e6, 1),
                       "repeat_identical": same}), flush=True)
-lib.ssnt_fwd_bwd_wide_split(0)
+lib.ssnt_fwd_bwd_wide_split(-1)
 lib.ssnt_fwd_bwd_wide_lanes(1)
 ident = torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 print(json.dumps({"split_vs_one_workgroup_bit_identical": ident}), flush=True)
