@@ -164,6 +164,23 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   xf* outr = reinterpret_cast<xf*>(inr + 2 * R * slot_bytes);
   xf* rows = LDS ? outr + 2 * kR2 * Up : reinterpret_cast<xf*>(a.workspace) + (size_t)b * T * Up;
   unsigned char* junk_lane = junk + 16 * K * lane;
+#ifdef SSNT_VAR_DESC
+  // study build: one descriptor per utterance tensor, rows as scalar offsets
+  const unsigned tub8 = (unsigned)(TU * 8), tub4 = (unsigned)(TU * 4);
+  const PosOff<K, 2, NV> po8(p0, U);
+  const PosOff<K, 1, NV> po4(p0, U);
+  auto so8 = [&](int s) { return (int)((unsigned)__builtin_amdgcn_readfirstlane(s) * (unsigned)U * 8u); };
+  auto so4 = [&](int s) { return (int)((unsigned)__builtin_amdgcn_readfirstlane(s) * (unsigned)U * 4u); };
+  const __amdgpu_buffer_rsrc_t g_r = brsrc(g, g ? tub8 : 0u);
+  const __amdgpu_buffer_rsrc_t go_r = brsrc(go, go ? tub4 : 0u);
+  const __amdgpu_buffer_rsrc_t la_r = brsrc(la, la ? tub4 : 0u);
+  const __amdgpu_buffer_rsrc_t lb_r = brsrc(lb, lb ? tub4 : 0u);
+#define SSNT_GST2(v, tensor, s) gst_s<K, 2, NV>(v, tensor##_r, po8, so8(s))
+#define SSNT_GST1(v, tensor, s) gst_s<K, 1, NV>(v, tensor##_r, po4, so4(s))
+#else
+#define SSNT_GST2(v, tensor, s) gst<K, 2, NV>(v, brsrc(tensor + (size_t)(s) * U * 2, U * 8u), p0)
+#define SSNT_GST1(v, tensor, s) gst<K, 1, NV>(v, brsrc(tensor + (size_t)(s) * U, U * 4u), p0)
+#endif
 
   auto fill_rows = [&](int from, int w0, int wstep) {  // zero grads / -inf debug rows
     float z[2 * K], ninf[K];
@@ -172,10 +189,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 #pragma unroll
     for (int j = 0; j < K; ++j) ninf[j] = -__builtin_inff();
     for (int s = from + w0; s < T; s += wstep) {
-      if (g) gst<K, 2, NV>(z, brsrc(g + (size_t)s * U * 2, U * 8u), p0);
-      if (go) gst<K, 1, NV>(z, brsrc(go + (size_t)s * U, U * 4u), p0);
-      if (la) gst<K, 1, NV>(ninf, brsrc(la + (size_t)s * U, U * 4u), p0);
-      if (lb) gst<K, 1, NV>(ninf, brsrc(lb + (size_t)s * U, U * 4u), p0);
+      if (g) SSNT_GST2(z, g, s);
+      if (go) SSNT_GST1(z, go, s);
+      if (la) SSNT_GST1(ninf, la, s);
+      if (lb) SSNT_GST1(ninf, lb, s);
     }
   };
   const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
@@ -400,7 +417,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
               if constexpr (OBS) gob[q] = xf_neg_post((A.m[q] * Bs.m[q]) * izm, ae + Bs.e[q]);
             }
           }
-          if (g && !EXP(1)) gst<K, 2, NV>(ge, brsrc(g + (size_t)s * U * 2, U * 8u), p0);
+          if (g && !EXP(1)) SSNT_GST2(ge, g, s);
           if constexpr (OBS) {
             if (go) gst<K, 1, NV>(gob, brsrc(go + (size_t)s * U, U * 4u), p0);
           }
@@ -447,6 +464,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     const unsigned tag0 = (d == 0 && c == 0 && b == 0 && a.loss_sum) ? sum_tag(a) : 0u;
     const int chain_end = d == 0 ? S - 1 : S;
     unsigned char* ring = inr + (size_t)d * R * slot_bytes;
+#ifdef SSNT_VAR_DESC
+    const __amdgpu_buffer_rsrc_t lt_r = brsrc(lt, tub8);
+#endif
     auto load = [&](int r, Item<K, OBS>& it) {
       if (EXP(6)) {
 #pragma unroll
@@ -454,7 +474,11 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         return;
       }
       const int row = min(max(d == 0 ? r : S - 1 - r, 0), T - 1);
+#ifdef SSNT_VAR_DESC
+      gld_s<K, 2, NV>(it.lt, lt_r, po8, so8(row));
+#else
       gld<K, 2, NV>(it.lt, brsrc(lt + (size_t)row * U * 2, U * 8u), p0);
+#endif
       if constexpr (OBS) {
         const int orow = min(row + 1, T - 1);
         gld<K, 1, NV>(it.ob, brsrc(lo + (size_t)orow * U, U * 4u), p0);
@@ -832,7 +856,9 @@ int launch_stream_k(const FwdBwdArgs& a, hipStream_t st, bool force_ws = false) 
              : launch_stream_kernel<K, OBS, false, NC, NH, RS, true>(a, head, st);
 }
 
-std::atomic<int> g_ring{0};  // A/B: 0 default rings; 16 / 32 ring slots with workspace rows (K = 2)
+#ifdef SSNT_AB
+std::atomic<int> g_ring{0};  // A/B build: 0 default rings; 16 / 32 ring slots with workspace rows (K = 2)
+#endif
 
 template <bool OBS>
 int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
@@ -850,11 +876,13 @@ int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
   return launch_stream_k<2, false, 3, 4>(a, st);
 #else
   if (a.U <= 64) return launch_stream_k<1, OBS, 3, 4>(a, st);
-  if constexpr (!OBS) {  // A/B (ssnt_fwd_bwd_stream_ring): deeper rings, rows in the workspace
+#ifdef SSNT_AB
+  if constexpr (!OBS) {  // A/B build (ssnt_fwd_bwd_stream_ring): deeper rings, rows in the workspace
     const int ring = g_ring.load(std::memory_order_relaxed);
     if (a.U > 64 && a.U <= 128 && ring == 16) return launch_stream_k<2, false, 3, 4, 16>(a, st, true);
     if (a.U > 64 && a.U <= 128 && ring == 32) return launch_stream_k<2, false, 3, 4, 32>(a, st, true);
   }
+#endif
   if (a.U <= 128) return launch_stream_k<2, OBS, SSNT_T_NC, SSNT_T_NH>(a, st);
   if (a.U <= 256) return launch_stream_k<4, OBS, 2, 2>(a, st);
   // K = 8 (U <= 512, configs[4]): the two-wave kernel. The streaming kernel needs 4-slot rings to
@@ -914,12 +942,14 @@ int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
   return a.log_obs ? launch_stream_obs<true>(a, st) : launch_stream_obs<false>(a, st);
 }
 
+#ifdef SSNT_AB
 int set_stream_ring(int r) {
   if (r != 0 && r != 16 && r != 32) return SSNT_ERR_INVALID_ARG;
   g_ring.store(r);
   return SSNT_OK;
 }
 int stream_ring() { return g_ring.load(std::memory_order_relaxed); }
+#endif
 
 void set_stream_mix(int m) {
 #ifdef SSNT_EXP
