@@ -12,9 +12,9 @@ ORACLE    := oracle/build/libssnt_oracle.so
 
 # -ffp-contract=off: the fwd-bwd arithmetic is specified op-by-op (no a*b+c contraction) so
 # the CPU oracle reproduces it bit for bit. Correctly rounded f32 division is HIP's default.
-HIPFLAGS  := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall \
+HIPFLAGS  := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden -Wall \
              -Wno-unused-function -I include -I $(CSRC)
-HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/fwd_bwd_stream.hip $(CSRC)/fwd_bwd_wide.hip $(CSRC)/v2_fwd_bwd.hip \
+HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/fwd_bwd_rows.hip $(CSRC)/fwd_bwd_stream.hip $(CSRC)/fwd_bwd_wide.hip $(CSRC)/v2_fwd_bwd.hip \
              $(CSRC)/decode.hip \
              $(CSRC)/fused_decode.hip $(CSRC)/capi.hip
 # the A/B build adds the kernels only its knobs reach (the pair kernel)

@@ -143,8 +143,8 @@ def main():
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--U", type=int, default=80)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--variant", type=int, default=0, help="fwd-bwd kernel variant (A/B; "
-                    "ssnt_fwd_bwd_set_variant): 0 default, 1 two-wave, 2 segmented")
+    ap.add_argument("--variant", type=int, default=0, help="fwd-bwd kernel variant (A/B build, "
+                    "include/ssnt_tts_c_ab.h): 0 the product's dispatch, 1 two-wave, 2 segmented")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse "
                     "the multi-rank path on a one-GPU box")
     args = ap.parse_args()
@@ -163,7 +163,8 @@ def main():
             torch.distributed.init_process_group(args.dist_backend)
 
     B, T, U = args.batch, args.T, args.U
-    if args.variant:
+    if args.variant:  # every later call goes through the A/B build (never the bench default)
+        S.use_ab().__enter__()
         assert S.load().ssnt_fwd_bwd_set_variant(args.variant) == 0
     lt = synth(B, T, U, seed=rank, dev=dev)
     sl = torch.full((B,), T, dtype=torch.int32, device=dev)

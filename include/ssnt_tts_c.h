@@ -120,19 +120,13 @@ int ssnt_version(char *buf, size_t len);
  * grad_obs (B,T,U) = d loss / d log_obs (NULL = skip); log_alpha / log_beta (B,T,U) debug
  * outputs (NULL = skip). Cells outside (S_b,P_b) get grad 0 and log-alpha/beta -inf.
  * Device variant: all pointers are device pointers; `stream` is a hipStream_t (NULL = legacy
- * default); `workspace` must hold ssnt_fwd_bwd_workspace_size() bytes -- 0 (NULL workspace)
- * when every row of the default dispatch stays in LDS (U <= 256 and T*U small enough), else the
- * segmented kernel's (T+1)*U rows per utterance; query it after ssnt_fwd_bwd_set_variant;
- * `status` (device int, may be NULL) receives error bits. Asynchronous. */
+ * default); `workspace` must hold ssnt_fwd_bwd_workspace_size() bytes -- always take the size
+ * from that query, never compute it: it is 0 (NULL workspace) when every row of the dispatched
+ * kernel stays in LDS (U <= 256 and T*U small enough), else the segmented kernel's rows
+ * ((T+1)*U xf per utterance) plus its hand-off counter block and hand-off rings, each padded to
+ * 256 B; `status` (device int, may be NULL) receives error bits. Asynchronous. The kernel is
+ * chosen from the shape and alignment alone (no process-wide state). */
 size_t ssnt_fwd_bwd_workspace_size(int batch, int max_steps, int max_pos);
-/* Kernel variant for the forward-backward: 0 = default dispatch (streaming kernel for U <= 256,
- * segmented kernel for longer rows, two-wave kernel for what neither takes); 1 = two-wave
- * kernel; 2 = segmented kernel at every U it takes (U <= 1024) -- 0, 1 and 2 are bit-identical;
- * 12 = the pair kernel first (U <= 128 without log_obs; two lattice rows per dependent chain
- * step, so its results follow the pair recurrence -- oracle ORACLE_PAIR, within the north_star
- * tolerance of the others, not bit-identical to them). Process-wide; env
- * SSNT_FWD_BWD_KERNEL=simple selects 1 at first use. For A/B timing and debugging. */
-int ssnt_fwd_bwd_set_variant(int variant);
 /* Name of the forward-backward kernel instance the calling thread's last ssnt_fwd_bwd* call
  * dispatched (e.g. "k_fwd_bwd_stream<K=2,OBS=0,LDS=1,NC=3,NH=4,RS=0,NV=0>"; launches of one call
  * joined by '+'), copied into buf (truncated to len); returns its full length. Lets a profile be

@@ -128,7 +128,12 @@ int ensure(size_t dbytes, size_t hbytes, const char* fn, bool abort_on_error) {
     g_ctx.hmap = nullptr;
     g_ctx.hcap = 0;
     const size_t cap = hbytes + hbytes / 2 + 4096;
-    if (hipHostMalloc(reinterpret_cast<void**>(&g_ctx.h), cap, hipHostMallocDefault) != hipSuccess) {
+    // coherent (fine-grained) and mapped: zero-copy plans are read and written by the kernel in
+    // place and the caller learns of completion from a flag word, not a stream synchronisation,
+    // so the kernel's stores must bypass the GPU caches (a coarse-grained buffer is only
+    // guaranteed coherent at synchronisation points)
+    if (hipHostMalloc(reinterpret_cast<void**>(&g_ctx.h), cap,
+                      hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
       if (abort_on_error) fail(fn, "hipHostMalloc failed");
       return SSNT_ERR_HIP;
     }
@@ -163,7 +168,12 @@ thread_local PhaseClock g_clk;
 // polled by the calling thread; 2 the same word written by a one-thread kernel launched after
 // it. A poll that sees nothing for kFlagTimeoutMs falls back to hipStreamSynchronize (which
 // then reports a failed kernel). Default measured per DESIGN.md 7.2 (tools/bench_step_symbols.py).
-std::atomic<int> g_sync_mode{2};
+#ifdef SSNT_AB
+std::atomic<int> g_sync_mode{2};  // A/B build: ssnt_set_host_sync
+int sync_mode() { return g_sync_mode.load(std::memory_order_relaxed); }
+#else
+constexpr int sync_mode() { return 2; }
+#endif
 constexpr double kFlagTimeoutMs = 5000.0;
 
 __global__ void k_flag(unsigned* f, unsigned v) {
@@ -195,7 +205,12 @@ bool wait_flag(int mode) {
 // zero-copy: the kernel reads its inputs from and writes its outputs to the pinned staging
 // buffer over the bus (no copies; launch + synchronise only). Default measured per DESIGN.md
 // (tools/bench_step_symbols.py); atomic, so concurrent callers never race on it.
-std::atomic<int> g_host_mode{1};
+#ifdef SSNT_AB
+std::atomic<int> g_host_mode{1};  // A/B build: ssnt_set_host_staging
+int host_mode() { return g_host_mode.load(std::memory_order_relaxed); }
+#else
+constexpr int host_mode() { return 1; }
+#endif
 constexpr size_t kZeroCopyMax = 1 << 20;  // plans up to this size may run zero-copy
 
 // Staging plan: a list of host arrays laid out in one buffer: inputs, the status word, then the
@@ -241,7 +256,7 @@ int stage_in(Plan& p, const char* fn, bool abort_on_error, size_t extra_device =
              bool allow_zero_copy = true) {
   p.layout();
   p.zero_copy = allow_zero_copy && extra_device == 0 && p.total <= kZeroCopyMax &&
-                g_host_mode.load(std::memory_order_relaxed) == 1;
+                host_mode() == 1;
   int rc = ensure(p.zero_copy ? 0 : Plan::align(p.total) + extra_device, p.total, fn,
                   abort_on_error);
   if (rc != SSNT_OK) return rc;
@@ -292,8 +307,8 @@ int stage_out(Plan& p, int launch_rc, const char* fn, bool abort_on_error) {
     const size_t lo = p.status_off, hi = p.total;
     e = hipMemcpyAsync(g_ctx.h + lo, g_ctx.d + lo, hi - lo, hipMemcpyDeviceToHost, g_ctx.stream);
   }
-  const int sync_mode = g_sync_mode.load(std::memory_order_relaxed);
-  if (e == hipSuccess && p.zero_copy && sync_mode != 0 && g_ctx.flag_h && wait_flag(sync_mode))
+  const int sm = sync_mode();
+  if (e == hipSuccess && p.zero_copy && sm != 0 && g_ctx.flag_h && wait_flag(sm))
     ;  // completion seen through the flag word: the outputs are in the staging buffer
   else if (e == hipSuccess)
     e = hipStreamSynchronize(g_ctx.stream);
@@ -330,6 +345,8 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 using namespace ssnt;
 
+// the C ABI is the library's only exported surface (everything else builds -fvisibility=hidden)
+#pragma GCC visibility push(default)
 extern "C" {
 
 const char* ssnt_status_string(int status) {
@@ -575,42 +592,44 @@ void tone_latent_levenshtein_edit_distance(const int* a, const int* b, const int
 
 // ------------------------------- extensions ---------------------------------------------------
 
-int ssnt_fwd_bwd_set_variant(int variant) { return set_fwd_bwd_variant(variant); }
-
 int ssnt_fwd_bwd_last_kernel(char* buf, size_t len) {
   const char* d = last_fwd_bwd_dispatch();
   if (buf && len) snprintf(buf, len, "%s", d);
   return (int)strlen(d);
 }
 
-// A/B of the host staging of the per-step reference symbols (tools/bench_step_symbols.py);
-// not part of the public header. 0 = copies, 1 = zero-copy. Returns the previous mode.
+// ---- A/B build only (-DSSNT_AB, lib/ab/libssnt_tts_c_ab.so; include/ssnt_tts_c_ab.h): the
+// process-wide kernel / staging / sync knobs and the diagnostic reads. The product library
+// exports none of them (tests/test_capi_exports.py).
+#ifdef SSNT_AB
+int ssnt_fwd_bwd_set_variant(int variant) { return set_fwd_bwd_variant(variant); }
+
+// host staging of the per-step reference symbols (tools/bench_step_symbols.py): 0 = copies,
+// 1 = zero-copy. Returns the previous mode.
 int ssnt_set_host_staging(int mode) {
   if (mode != 0 && mode != 1) return -1;
   return g_host_mode.exchange(mode);
 }
 
-// A/B of how the per-step reference symbols wait for their kernel (g_sync_mode); not part of
-// the public header. Returns the previous mode.
+// how the per-step reference symbols wait for their kernel (g_sync_mode). Returns the previous
+// mode.
 int ssnt_set_host_sync(int mode) {
   if (mode < 0 || mode > 2) return -1;
   return g_sync_mode.exchange(mode);
 }
 
-// A/B of the fused decodes' step ordering (tools, tests): -1 default, 0 full rank, 1 selection;
-// not part of the public header.
+// the fused decodes' step ordering: -1 default, 0 full rank, 1 selection
 int ssnt_fused_decode_select(int mode) { return set_fused_decode_select(mode); }
 
-// A/B of the long-row kernel's lane width (tools, tests); not part of the public header.
+// the long-row kernel's lane width
 int ssnt_fwd_bwd_wide_lanes(int k) { return set_fwd_bwd_wide_lanes(k); }
-// A/B of the long-row kernel's workgroup split (-1 auto, 0 one workgroup per direction, 1 two
-// whenever a direction has 2+ segments); not part of the public header.
+// the long-row kernel's workgroup split (-1 auto, 0 one workgroup per direction, 1 two
+// whenever a direction has 2+ segments)
 int ssnt_fwd_bwd_wide_split(int mode) { return set_fwd_bwd_wide_split(mode); }
-// A/B of the streaming kernel's ring depth (16 / 32 slots, rows in the workspace; 0 default);
-// not part of the public header.
+// the streaming kernel's ring depth (16 / 32 slots, rows in the workspace; 0 default)
 int ssnt_fwd_bwd_stream_ring(int r) { return set_stream_ring(r); }
 
-// Per-step symbol latency breakdown (tools/bench_step_symbols.py); not part of the public header.
+// Per-step symbol latency breakdown (tools/bench_step_symbols.py).
 // enable = 1 resets and starts the calling thread's phase clock; 0 stops it and writes the mean
 // microseconds of its 5 phases (PhaseClock) to out[0..4]; returns the number of calls timed.
 int ssnt_diag_step_clock(int enable, double* out) {
@@ -642,10 +661,12 @@ int ssnt_diag_null_launch(int reps, double* out) {
   return reps;
 }
 
-// diagnostic builds (make lib-diag) only; not part of the public header
+// in-kernel stamps of the diagnostic builds (make lib-diag / lib-exp; -1 otherwise)
 int ssnt_diag_read(void* host, size_t bytes) { return diag_read(host, bytes); }
 int ssnt_diag_decode_read(void* host, size_t bytes) { return diag_decode_read(host, bytes); }
 
+
+#endif  // SSNT_AB
 
 size_t ssnt_fwd_bwd_sum_state_size(int batch) { return batch > 0 ? fwd_bwd_sum_state_bytes(batch) : 0; }
 
@@ -911,3 +932,4 @@ int ssnt_levenshtein_edit_distance_device(const int* a, const int* b, const int*
 }
 
 }  // extern "C"
+#pragma GCC visibility pop

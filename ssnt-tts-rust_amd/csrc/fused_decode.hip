@@ -723,15 +723,17 @@ inline int last_error() { return hipGetLastError() == hipSuccess ? SSNT_OK : SSN
 
 constexpr size_t kMaxLds = 150 * 1024;
 
-// ordering of the register kernel's step: -1 the default per variant, 0 full rank, 1 selection
-// (A/B hook ssnt_fused_decode_select; both give identical outputs)
+// ordering of the register kernel's step: the full rank. The selection ordering (SEL) is
+// bit-identical and measured slower at every BASELINE shape; it is compiled
+// only into the A/B build (-DSSNT_AB: ssnt_fused_decode_select 0 full rank, 1 selection).
+#ifdef SSNT_AB
 std::atomic<int> g_select{-1};
-bool use_select(Variant v) {
-  const int m = g_select.load(std::memory_order_relaxed);
-  if (m >= 0) return m == 1;
-  (void)v;
-  return false;  // measured slower at every BASELINE shape
-}
+bool use_select() { return g_select.load(std::memory_order_relaxed) == 1; }
+#define SSNT_SEL_OR_RANK(sel, RANK, SELK) ((sel) ? (SELK) : (RANK))
+#else
+constexpr bool use_select() { return false; }
+#define SSNT_SEL_OR_RANK(sel, RANK, SELK) (RANK)
+#endif
 
 template <typename K>
 int launch_with_lds(K kernel, size_t lds, int B, hipStream_t st, const FusedDecodeArgs& a,
@@ -757,19 +759,20 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
     const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged, whole).total;
     if (lds > kMaxLds) return SSNT_ERR_UNSUPPORTED;
     const int h = hist_lds ? 1 : 0;
-    const bool sel = use_select(V);
+    const bool sel = use_select();
+    (void)sel;
     auto go = [&](auto kw, auto kc) {  // (NMAX, WHOLE) instance
       constexpr int NM = decltype(kw)::value;
       constexpr bool WH = decltype(kc)::value;
       if (!staged) {  // only v1 rows can be too long to stage
         if constexpr (V == Variant::V1) {
-          return sel ? launch_with_lds(k_fused_reg<V, false, 64, WH, true>, lds, a.B, st, a, h)
-                     : launch_with_lds(k_fused_reg<V, false, 64, WH, false>, lds, a.B, st, a, h);
+          return SSNT_SEL_OR_RANK(sel, launch_with_lds(k_fused_reg<V, false, 64, WH, false>, lds, a.B, st, a, h),
+                                  launch_with_lds(k_fused_reg<V, false, 64, WH, true>, lds, a.B, st, a, h));
         }
         return (int)SSNT_ERR_UNSUPPORTED;
       }
-      return sel ? launch_with_lds(k_fused_reg<V, true, NM, WH, true>, lds, a.B, st, a, h)
-                 : launch_with_lds(k_fused_reg<V, true, NM, WH, false>, lds, a.B, st, a, h);
+      return SSNT_SEL_OR_RANK(sel, launch_with_lds(k_fused_reg<V, true, NM, WH, false>, lds, a.B, st, a, h),
+                              launch_with_lds(k_fused_reg<V, true, NM, WH, true>, lds, a.B, st, a, h));
     };
     auto pick = [&](auto kc) {
       if (n <= 8) return go(std::integral_constant<int, 8>{}, kc);
@@ -809,11 +812,13 @@ int diag_decode_read(void* host, size_t bytes) {
 #endif
 }
 
+#ifdef SSNT_AB
 int set_fused_decode_select(int mode) {
   if (mode < -1 || mode > 1) return SSNT_ERR_INVALID_ARG;
   g_select.store(mode);
   return SSNT_OK;
 }
+#endif
 
 int launch_fused_decode(const FusedDecodeArgs& a, hipStream_t st) {
   if (a.B < 0 || a.W <= 0 || a.T <= 0 || !a.src || !a.input_length || !a.prediction ||

@@ -324,12 +324,13 @@ int launch_simple(const FwdBwdArgs& a, hipStream_t st) {
   return SSNT_ERR_UNSUPPORTED;
 }
 
-// 0 default: the streaming kernel (fwd_bwd_stream.hip), else the segmented kernel, else the
-// two-wave kernel; 1 two-wave kernel only; 2 segmented kernel; 3 the default with the pair
-// kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs; bit-exact with the oracle's pair
-// recurrence, measured slower than the streaming kernel: DESIGN.md 5.1a). Process-wide A/B
-// switch: read from the environment once (SSNT_FWD_BWD_KERNEL=simple selects 1), atomic so
-// concurrent callers never race on it.
+// Kernel choice. The product dispatches by shape only (rows kernel, else the streaming kernel,
+// else the segmented kernel, else the two-wave kernel). The A/B build (-DSSNT_AB, `make lib-ab`;
+// tests and tools only) adds a process-wide override: 1 two-wave kernel only, 2 segmented
+// kernel, 3 the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs; its own rounding
+// order, oracle ORACLE_PAIR; measured slower: DESIGN.md 5.1a), 4 the streaming kernel where the
+// rows kernel would run; SSNT_FWD_BWD_KERNEL=simple selects 1 there.
+#ifdef SSNT_AB
 std::atomic<int> g_variant{0};
 std::once_flag g_variant_env;
 int variant() {
@@ -339,6 +340,9 @@ int variant() {
   });
   return g_variant.load(std::memory_order_relaxed);
 }
+#else
+constexpr int variant() { return 0; }
+#endif
 
 thread_local char t_dispatch[160];
 
@@ -356,8 +360,9 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
   // 0 when the default dispatch keeps every row in LDS whatever the call brings: U <= 256, the
   // streaming kernel's rows fit beside its rings with or without log_obs and with the narrow
   // form's padded rows, and the two-wave kernel (what takes 4-byte-aligned tensors)
-  // fits its rows too. (The segmented kernel, variant 2, always needs the workspace.)
-  if (variant() != 2 && stream_ring() == 0 && U <= 256) {
+  // fits its rows too. (The A/B build's forced segmented kernel, pair kernel and deep rings
+  // always get the workspace.)
+  if (variant() == 0 && stream_ring() == 0 && U <= 256) {
     const int K = U <= 64 ? 1 : U <= 128 ? 2 : 4;
     const size_t Up = (size_t)K * ((U + K - 1) / K);
     const size_t rows = (size_t)T * Up * sizeof(xf);
@@ -365,33 +370,32 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
     const size_t h0 = stream_head_bytes(K, U, false), h1 = stream_head_bytes(K, U, true);
     const bool stream_lds = (h0 > h1 ? h0 : h1) + rows <= kLdsBudget;
     const bool simple_lds = (size_t)(64 * K + 2) * sizeof(xf) + (size_t)T * U * sizeof(xf) <= kLdsBudget;
-    // the pair kernel (U <= 128, no log_obs) keeps half the rows beside larger rings
-    const bool pair_lds = variant() != 3 || U > 128 ||
-                          pair_head_bytes(K, U) + pair_storage_bytes(K, T, U) <= kLdsBudget;
-    if (stream_lds && simple_lds && pair_lds) return 0;
+    if (stream_lds && simple_lds) return 0;
   }
   // the segmented kernel keeps its rows (plus beta at the cut) in the workspace at every T; one
-  // size serves every kernel variant (the two-wave kernel needs B*T*U xf at most)
-  // (the streaming kernel's narrow form pads rows to whole lane slices: U + 3 at most)
+  // size serves every kernel (the two-wave kernel needs B*T*U xf at most; the streaming
+  // kernel's narrow form pads rows to whole lane slices: U + 3 at most)
   const size_t wide = fwd_bwd_wide_workspace_bytes(B, T, U);
   const size_t stream = (size_t)B * T * ((size_t)U + 3) * sizeof(xf);
   return wide > stream ? wide : stream;
 }
 
+#ifdef SSNT_AB
 int set_fwd_bwd_variant(int v) {
-  // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel (fwd_bwd_wide.hip) at every U it
-  // takes; 3..11 (SSNT_EXP builds only): streaming kernel with another wave mix / ring /
-  // publication period (tuning)
-  // takes; 12: the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs)
-  if (v < 0 || v > 12) return SSNT_ERR_INVALID_ARG;
+  // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel at every U it takes; 3..11
+  // (SSNT_EXP builds only): streaming kernel with another wave mix / ring / publication period;
+  // 12: the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs); 13: the streaming
+  // kernel where the rows kernel would run (fwd_bwd_stream.hip)
+  if (v < 0 || v > 13) return SSNT_ERR_INVALID_ARG;
 #ifndef SSNT_EXP
-  if (v >= 3 && v != 12) return SSNT_ERR_UNSUPPORTED;
+  if (v >= 3 && v < 12) return SSNT_ERR_UNSUPPORTED;
 #endif
   variant();  // the environment is read once, before any explicit choice
-  g_variant.store(v == 12 ? 3 : v >= 3 ? 0 : v);
-  set_stream_mix(v >= 3 && v != 12 ? v - 2 : 0);
+  g_variant.store(v == 12 ? 3 : v == 13 ? 4 : v >= 3 ? 0 : v);
+  set_stream_mix(v >= 3 && v < 12 ? v - 2 : 0);
   return SSNT_OK;
 }
+#endif
 
 namespace {
 __global__ __launch_bounds__(64) void k_loss_sum(const float* loss, int B, float* out) {
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(64) void k_loss_sum(const float* loss, int B, float
 
 int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
   summed = false;
-  if (variant() == 0 || variant() == 3) {
+  if (variant() == 0 || variant() == 3 || variant() == 4) {
     FwdBwdArgs x = a;
 #ifdef SSNT_EXP
     const char* ee = getenv("SSNT_EXP");
@@ -409,7 +413,10 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
 #endif
     if (!a.sum_state) x.loss_sum = nullptr;
     int rc = SSNT_ERR_UNSUPPORTED;
+#ifdef SSNT_AB
     if (variant() == 3 && stream_ring() == 0) rc = launch_fwd_bwd_pair(x, st);
+#endif
+    if (rc == SSNT_ERR_UNSUPPORTED && variant() == 0 && stream_ring() == 0) rc = launch_fwd_bwd_rows(x, st);
     if (rc == SSNT_ERR_UNSUPPORTED) rc = launch_fwd_bwd_stream(x, st);
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;
@@ -433,6 +440,7 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
 size_t fwd_bwd_sum_state_bytes(int B) { return kSumGranuleOffset + 8 * (size_t)(B > 0 ? B : 0); }
 
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t st) {
+  t_dispatch[0] = 0;  // (an argument error or an empty batch dispatches nothing)
   if (a.B < 0 || a.T <= 0 || a.U <= 0 || !a.log_trans || !a.step_len || !a.pos_len || !a.loss)
     return SSNT_ERR_INVALID_ARG;
   if (a.grad_obs && !a.log_obs) return SSNT_ERR_INVALID_ARG;

@@ -130,13 +130,14 @@ __device__ __forceinline__ void wait_ge(const int* p, int target, int* status) {
   }
 }
 
-// the same on a global counter written by another workgroup (relaxed agent-scope polls)
+// the same on a global counter written by another workgroup (relaxed agent-scope polls);
+// -1 when the bound expired (the caller poisons what it forwards)
 __device__ __forceinline__ int gwait_ge(const int* p, int target, int* status) {
   int v = gctr_ld(p);
   for (int n = 0; v < target; ++n) {
     if (n > kSpinMax) {
       if (status && (threadIdx.x & 63) == 0) atomicOr(status, kStatusTimeout);
-      return target;
+      return -1;
     }
     __builtin_amdgcn_s_sleep(2);
     v = gctr_ld(p);
@@ -423,12 +424,18 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
       }
     } else {  // receiver: global -> the first compute wave's upstream ring
       int seen = 0;
+      bool dead = false;  // the upstream workgroup never published: forward NaN from here on, so
+                          // the utterance's loss and gradients are NaN, never plausible values
       for (int i0 = 0; i0 < n; i0 += kBS) {
         const int i1 = min(i0 + kBS, n);
-        if (seen < i1) seen = gwait_ge(ctr, i1, a.status);
+        if (!dead && seen < i1) {
+          seen = gwait_ge(ctr, i1, a.status);
+          dead = seen < 0;
+        }
         asm volatile("" ::: "memory");  // the payload loads stay behind the poll
         f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
         if (lane < kL) v = rbuf_ld4(gr, (i0 + 2 * lane) * 8, 0, kSC1);
+        if (dead) v = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
         wait_ge(&ctl.cons[0], i1 - kRB, a.status);
         wbar();
         if (lane < kL) *reinterpret_cast<f32x4*>(&ctl.bnd[kProxy][i0 % kRB + 2 * lane]) = v;
@@ -795,7 +802,12 @@ inline WideLayout wide_layout(int B, int T, int U) {
 // the heaviest workgroups (K = 2, 8 waves) when 4B <= CUs -- measured per shape, DESIGN.md 5.2
 // (configs[4], B=64 U=400: one workgroup 604 vs split 637 us; B=32: 565 vs 511; B=64 U=1024:
 // 868 vs 749); 0 never; 1 whenever NW >= 2
-std::atomic<int> g_wide_split{-1};
+#ifdef SSNT_AB
+std::atomic<int> g_wide_split{-1};  // A/B build: ssnt_fwd_bwd_wide_split
+int wide_split_mode() { return g_wide_split.load(std::memory_order_relaxed); }
+#else
+constexpr int wide_split_mode() { return -1; }
+#endif
 
 int device_cus() {
   static std::atomic<int> cus[64];
@@ -821,7 +833,7 @@ int launch_wide(const FwdBwdArgs& a, hipStream_t st) {
   gd.gring = reinterpret_cast<xf*>(ws + l.ctr);
   gd.RL = a.T + 32;  // whole blocks of up to 32 steps
   gd.rows = reinterpret_cast<xf*>(ws + l.ctr + l.gring);
-  const int mode = g_wide_split.load(std::memory_order_relaxed);
+  const int mode = wide_split_mode();
   bool split = false;
   if (NW >= 2 && mode == 1) {
     split = true;
@@ -853,7 +865,13 @@ int launch_wide_k(const FwdBwdArgs& a, hipStream_t st) {
   return dbg ? launch_wide<K, false, true>(a, st) : launch_wide<K, false, false>(a, st);
 }
 
-std::atomic<int> g_wide_k{1};  // positions per lane (A/B hook ssnt_fwd_bwd_wide_lanes; 1 default)
+// positions per lane: 1 up to U = 512 (A/B build: ssnt_fwd_bwd_wide_lanes forces 2)
+#ifdef SSNT_AB
+std::atomic<int> g_wide_k{1};
+int wide_lanes() { return g_wide_k.load(std::memory_order_relaxed); }
+#else
+constexpr int wide_lanes() { return 1; }
+#endif
 
 }  // namespace
 
@@ -873,10 +891,11 @@ int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t st, bool any_u) {
     return SSNT_ERR_WORKSPACE;
   // one descriptor per utterance tensor, position offsets up to 2^31 (row helpers)
   if ((size_t)(a.T + 1) * a.U * 8 >= ((size_t)1 << 31)) return SSNT_ERR_UNSUPPORTED;
-  const bool k1 = g_wide_k.load(std::memory_order_relaxed) == 1 && a.U <= 64 * kMaxNW;
+  const bool k1 = wide_lanes() == 1 && a.U <= 64 * kMaxNW;
   return k1 ? launch_wide_k<1>(a, st) : launch_wide_k<2>(a, st);
 }
 
+#ifdef SSNT_AB
 int set_fwd_bwd_wide_lanes(int k) {
   if (k != 1 && k != 2) return SSNT_ERR_INVALID_ARG;
   g_wide_k.store(k);
@@ -888,5 +907,6 @@ int set_fwd_bwd_wide_split(int mode) {
   g_wide_split.store(mode);
   return SSNT_OK;
 }
+#endif
 
 }  // namespace ssnt

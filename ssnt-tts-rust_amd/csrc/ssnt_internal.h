@@ -40,23 +40,33 @@ struct FwdBwdArgs {
 size_t fwd_bwd_workspace_bytes(int B, int T, int U);
 size_t fwd_bwd_sum_state_bytes(int B);  // 64 + 8 B
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
-int set_fwd_bwd_variant(int v);
+// rows kernel (fwd_bwd_rows.hip; the default for U <= 128 without log_obs, U % K == 0, 16-byte
+// aligned tensors, rows within LDS): SSNT_ERR_UNSUPPORTED for shapes it does not take
+int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t stream);
 // streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t stream);
-void set_stream_mix(int m);  // tuning only
-int set_stream_ring(int r);  // A/B only: 0 default, 16 / 32 ring slots with workspace rows
-int stream_ring();
+void set_stream_mix(int m);  // tuning only (SSNT_EXP builds)
 // segmented kernel (fwd_bwd_wide.hip): long rows (256 < U <= 1024), or any U <= 1024 when
 // any_u; SSNT_ERR_UNSUPPORTED for other shapes
 int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t stream, bool any_u);
 size_t fwd_bwd_wide_workspace_bytes(int B, int T, int U);
-int set_fwd_bwd_wide_lanes(int k);  // A/B: positions per lane of the long-row kernel (1 or 2)
-int set_fwd_bwd_wide_split(int mode);  // A/B: two workgroups per direction (-1 auto, 0 off, 1 on)
 size_t stream_head_bytes(int K, int U, bool obs, int ring = 0);  // LDS bytes besides the lattice rows
+// Process-wide A/B knobs and the kernels only they reach: the A/B build (-DSSNT_AB, `make
+// lib-ab`, lib/ab/libssnt_tts_c_ab.so; tests and tools) only. The product dispatches by shape.
+#ifdef SSNT_AB
+int set_fwd_bwd_variant(int v);
+int set_stream_ring(int r);  // 0 default, 16 / 32 ring slots with workspace rows
+int stream_ring();
+int set_fwd_bwd_wide_lanes(int k);  // positions per lane of the long-row kernel (1 or 2)
+int set_fwd_bwd_wide_split(int mode);  // two workgroups per direction (-1 auto, 0 off, 1 on)
 // pair kernel (fwd_bwd_pair.hip): U <= 128 without log_obs; SSNT_ERR_UNSUPPORTED otherwise
 int launch_fwd_bwd_pair(const FwdBwdArgs& a, hipStream_t stream);
 size_t pair_head_bytes(int K, int U);            // LDS bytes besides the stored rows
 size_t pair_storage_bytes(int K, int T, int U);  // stored rows of one utterance
+int set_fused_decode_select(int mode);  // -1 default, 0 full rank, 1 selection
+#else
+constexpr int stream_ring() { return 0; }
+#endif
 int diag_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only (tools/diag_fwd_bwd.py)
 // the fwd-bwd kernel instance this thread dispatched last ("k_fwd_bwd_stream<K=2,...>"; one
 // name per launch of a multi-launch kernel, joined by '+'); for bench.py's profile check
@@ -148,7 +158,6 @@ struct FusedDecodeArgs {
   int* status;
 };
 int launch_fused_decode(const FusedDecodeArgs& a, hipStream_t stream);
-int set_fused_decode_select(int mode);  // A/B: -1 default, 0 full rank, 1 selection
 int diag_decode_read(void* host, size_t bytes);  // -DSSNT_DIAG builds only
 
 int launch_extract_best(int B, int W, int U, const int* best_final_branch, const int* beam_branch,

@@ -17,7 +17,7 @@ import ctypes
 
 import torch
 
-from ._lib import SsntError, last_fwd_bwd_kernel, load, status_string  # noqa: F401
+from ._lib import SsntError, last_fwd_bwd_kernel, load, load_ab, status_string, use_ab  # noqa: F401
 
 FLAG_TERMINAL_EMIT = 1
 FLAG_ZERO_INFINITY = 2

@@ -11,6 +11,9 @@ from pathlib import Path
 
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("SSNT_TTS_C_LIB", _PKG_ROOT / "lib" / "libssnt_tts_c.so"))
+# the A/B build (make lib-ab; include/ssnt_tts_c_ab.h): the product plus process-wide kernel /
+# staging / sync knobs -- tests and tools only, never the product path
+AB_LIB_PATH = _PKG_ROOT / "lib" / "ab" / "libssnt_tts_c_ab.so"
 
 c_int, c_float, c_bool, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_float, ctypes.c_bool,
                                              ctypes.c_size_t, ctypes.c_void_p)
@@ -35,7 +38,6 @@ SIGNATURES = {
     "ssnt_version": (c_int, [ctypes.c_char_p, c_size_t]),
     "ssnt_fwd_bwd_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "ssnt_fwd_bwd_sum_state_size": (c_size_t, [c_int]),
-    "ssnt_fwd_bwd_set_variant": (c_int, [c_int]),
     "ssnt_fwd_bwd_last_kernel": (c_int, [ctypes.c_char_p, c_size_t]),
     "ssnt_fwd_bwd_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
                                     c_size_t, P, P]),
@@ -66,33 +68,90 @@ SIGNATURES = {
     "ssnt_levenshtein_edit_distance_device": (c_int, [P, P, P, P, c_int, c_int, P, P]),
 }
 
-_lib = None
+# include/ssnt_tts_c_ab.h: the A/B build's extra symbols
+AB_SIGNATURES = {
+    "ssnt_fwd_bwd_set_variant": (c_int, [c_int]),
+    "ssnt_fwd_bwd_wide_lanes": (c_int, [c_int]),
+    "ssnt_fwd_bwd_wide_split": (c_int, [c_int]),
+    "ssnt_fwd_bwd_stream_ring": (c_int, [c_int]),
+    "ssnt_fused_decode_select": (c_int, [c_int]),
+    "ssnt_set_host_staging": (c_int, [c_int]),
+    "ssnt_set_host_sync": (c_int, [c_int]),
+    "ssnt_diag_step_clock": (c_int, [c_int, c_void_p]),
+    "ssnt_diag_null_launch": (c_int, [c_int, c_void_p]),
+    "ssnt_diag_read": (c_int, [c_void_p, c_size_t]),
+    "ssnt_diag_decode_read": (c_int, [c_void_p, c_size_t]),
+}
+
+_lib = None      # the product library
+_ab = None       # the A/B build, loaded on demand
+_active = None   # what the mirror calls (the product unless inside use_ab())
+
+
+def _bind(path: Path, sigs) -> ctypes.CDLL:
+    try:
+        import torch  # noqa: F401  (shares the HIP runtime)
+    except ImportError:
+        pass
+    if not path.exists():
+        raise RuntimeError(f"{path.name} not found at {path}: build it with `make` "
+                           "(there is no CPU fallback)")
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
 
 
 def load(require_gpu: bool = False):
-    """Load and bind libssnt_tts_c.so. `import torch` first so the library binds to the same
-    libamdhip64 instance torch uses (same soname)."""
+    """Load and bind libssnt_tts_c.so (`import torch` first so the library binds to the same
+    libamdhip64 instance torch uses). Inside use_ab() this returns the A/B build instead."""
     global _lib
     if _lib is None:
-        try:
-            import torch  # noqa: F401  (shares the HIP runtime)
-        except ImportError:
-            pass
-        if not LIB_PATH.exists():
-            raise RuntimeError(
-                f"libssnt_tts_c.so not found at {LIB_PATH}: build it with `make lib` "
-                "(there is no CPU fallback)")
-        lib = ctypes.CDLL(str(LIB_PATH))
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = lib
+        _lib = _bind(LIB_PATH, SIGNATURES)
     if require_gpu:
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("libssnt_tts_c: no GPU visible (there is no CPU fallback)")
-    return _lib
+    return _active if _active is not None else _lib
+
+
+def load_ab():
+    """The A/B build (lib/ab/libssnt_tts_c_ab.so): every product symbol plus the knobs of
+    include/ssnt_tts_c_ab.h. Own soname, so it loads beside the product library."""
+    global _ab
+    if _ab is None:
+        _ab = _bind(AB_LIB_PATH, {**SIGNATURES, **AB_SIGNATURES})
+    return _ab
+
+
+class use_ab:
+    """Context manager: the mirror functions call the A/B build while inside (tests that force a
+    kernel or a host mode). Nestable; the outermost exit resets every knob to its default."""
+    _depth = 0
+
+    def __enter__(self):
+        global _active
+        load()
+        _active = load_ab()
+        use_ab._depth += 1
+        return _active
+
+    def __exit__(self, *exc):
+        global _active
+        use_ab._depth -= 1
+        if use_ab._depth == 0:
+            ab = load_ab()
+            ab.ssnt_fwd_bwd_set_variant(0)
+            ab.ssnt_fwd_bwd_wide_lanes(1)
+            ab.ssnt_fwd_bwd_wide_split(-1)
+            ab.ssnt_fwd_bwd_stream_ring(0)
+            ab.ssnt_fused_decode_select(-1)
+            ab.ssnt_set_host_staging(1)
+            ab.ssnt_set_host_sync(2)
+            _active = None
+        return False
 
 
 def last_fwd_bwd_kernel() -> str:

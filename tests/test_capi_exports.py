@@ -9,7 +9,9 @@ import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
 HEADER = ROOT / "include" / "ssnt_tts_c.h"
+AB_HEADER = ROOT / "include" / "ssnt_tts_c_ab.h"
 LIB = ROOT / "ssnt-tts-rust_amd" / "lib" / "libssnt_tts_c.so"
+AB_LIB = ROOT / "ssnt-tts-rust_amd" / "lib" / "ab" / "libssnt_tts_c_ab.so"
 
 REFERENCE_SYMBOLS = [
     "ssnt_tts_beam_search_decode", "ssnt_extract_best_beam_branch",
@@ -18,8 +20,8 @@ REFERENCE_SYMBOLS = [
 ]
 
 
-def header_functions():
-    txt = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+def header_functions(header=HEADER):
+    txt = re.sub(r"/\*.*?\*/", "", header.read_text(), flags=re.S)
     txt = re.sub(r"#.*", "", txt)
     names = re.findall(r"\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", txt)
     return sorted(set(n for n in names if n not in ("if", "while", "sizeof")))
@@ -31,21 +33,48 @@ def test_header_declares_reference_symbols():
         assert s in fns
 
 
-def test_library_exports_every_header_symbol():
-    assert LIB.exists(), "build the library first (make lib)"
-    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True,
+def _exported(lib):
+    assert lib.exists(), f"build the library first (make): {lib}"
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib)], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(line.split()[-1] for line in out.splitlines() if " T " in line)
+    return set(line.split()[-1] for line in out.splitlines() if " T " in line)
+
+
+def test_library_exports_every_header_symbol():
+    exported = _exported(LIB)
     missing = [f for f in header_functions() if f not in exported]
     assert not missing, f"declared but not exported: {missing}"
 
 
+def test_product_exports_no_ab_knob():
+    # the product's exported surface is the reference's 7 symbols plus the
+    # extensions dispatch uses; the process-wide A/B knobs and diagnostics live only in the A/B
+    # build (include/ssnt_tts_c_ab.h), so no caller can flip another thread's kernel
+    exported = _exported(LIB)
+    ab = header_functions(AB_HEADER)
+    assert ab and not set(ab) & set(header_functions())
+    leaked = sorted(f for f in exported if f in ab or "set_variant" in f or "diag" in f)
+    assert not [f for f in exported if f.startswith("_Z")], "C++ internals exported (-fvisibility=hidden)"
+    assert not leaked, f"A/B symbols in the product library: {leaked}"
+    assert sorted(f for f in exported if f.startswith(("ssnt_", "tone_"))) == header_functions()
+
+
+def test_ab_library_exports_both_headers():
+    exported = _exported(AB_LIB)
+    missing = [f for f in header_functions() + header_functions(AB_HEADER) if f not in exported]
+    assert not missing, f"declared but not exported by the A/B build: {missing}"
+
+
 def test_ctypes_binding_matches_header():
-    from ssnt_tts_amd._lib import SIGNATURES, load
+    from ssnt_tts_amd._lib import AB_SIGNATURES, SIGNATURES, load, load_ab
     assert sorted(SIGNATURES) == header_functions()
+    assert sorted(AB_SIGNATURES) == header_functions(AB_HEADER)
     lib = load()  # dlopen only; no HIP call
     for name in SIGNATURES:
         assert getattr(lib, name) is not None
+    ab = load_ab()
+    for name in AB_SIGNATURES:
+        assert getattr(ab, name) is not None
 
 
 def test_reference_symbols_are_unmangled_c():
@@ -81,20 +110,16 @@ def test_mirror_fails_loudly_without_gpu():
 def test_segmented_workspace_query_covers_the_handoff_block():
     # host-only queries (no HIP call): the long-row kernel's workspace = the hand-off counter
     # block + the global hand-off rings + its rows (fwd_bwd_wide.hip wide_layout), each piece
-    # padded to 256 B; the A/B hook for its workgroup split takes -1 / 0 / 1 only
-    import ctypes
-    from ssnt_tts_amd._lib import load
+    # padded to 256 B; the A/B build's hook for its workgroup split takes -1 / 0 / 1 only
+    from ssnt_tts_amd._lib import load, load_ab
     lib = load()
-    lib.ssnt_fwd_bwd_workspace_size.restype = ctypes.c_size_t
-    lib.ssnt_fwd_bwd_workspace_size.argtypes = [ctypes.c_int] * 3
     r256 = lambda x: (x + 255) & ~255  # noqa: E731
     for B, T, U in [(64, 2000, 400), (2, 1030, 1024), (3, 33, 300), (1, 1, 257)]:
         wide = r256(16 * B) + r256(B * 2 * (T + 32) * 8) + B * (T + 1) * U * 8
         stream = B * T * (U + 3) * 8
         assert lib.ssnt_fwd_bwd_workspace_size(B, T, U) == max(wide, stream), (B, T, U)
-    lib.ssnt_fwd_bwd_wide_split.restype = ctypes.c_int
-    lib.ssnt_fwd_bwd_wide_split.argtypes = [ctypes.c_int]
+    ab = load_ab()
     for bad in (-2, 2, 7):
-        assert lib.ssnt_fwd_bwd_wide_split(bad) != 0
+        assert ab.ssnt_fwd_bwd_wide_split(bad) != 0
     for ok in (0, 1, -1):
-        assert lib.ssnt_fwd_bwd_wide_split(ok) == 0
+        assert ab.ssnt_fwd_bwd_wide_split(ok) == 0

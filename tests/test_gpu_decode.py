@@ -28,13 +28,14 @@ def _eq(gpu_out, ref, keys, ctx=""):
 
 @pytest.fixture(params=[0, 1], ids=["rank", "select"])
 def select_mode(request, gpu):
-    """The fused decodes' two step orderings (full rank / selection) must give identical outputs."""
-    import ctypes
-    lib = gpu.load()
-    lib.ssnt_fused_decode_select.restype = ctypes.c_int
-    assert lib.ssnt_fused_decode_select(request.param) == 0
-    yield request.param
-    lib.ssnt_fused_decode_select(-1)
+    """The fused decodes' two step orderings (full rank: the product; selection: forced through
+    the A/B build, include/ssnt_tts_c_ab.h) must give identical outputs."""
+    if request.param == 0:
+        yield 0
+        return
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_fused_decode_select(1) == 0
+        yield 1
 
 
 @pytest.fixture(params=[0, 1, 2], ids=["sync", "writevalue", "flagkernel"])
@@ -42,14 +43,12 @@ def host_sync(request, gpu):
     """The per-step host symbols' three ways of waiting for their kernel (hipStreamSynchronize,
     a hipStreamWriteValue32 completion word, a completion word written by a flag kernel) must
     return identical outputs."""
-    import ctypes
-    lib = gpu.load()
-    lib.ssnt_set_host_sync.restype = ctypes.c_int
-    lib.ssnt_set_host_sync.argtypes = [ctypes.c_int]
-    prev = lib.ssnt_set_host_sync(request.param)
-    assert prev >= 0
-    yield request.param
-    lib.ssnt_set_host_sync(prev)
+    if request.param == 2:  # the product's own mode
+        yield 2
+        return
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_set_host_sync(request.param) >= 0
+        yield request.param
 
 
 V1_KEYS = ("prediction", "log_prob", "next_t", "next_u", "next_is_finished", "beam_branch")

@@ -24,13 +24,14 @@ def _t(x):
 
 @pytest.fixture(autouse=True, params=[0, 1], ids=["rank", "select"])
 def select_mode(request, gpu):
-    """The fused decodes' two step orderings (full rank / selection) must give identical outputs."""
-    import ctypes
-    lib = gpu.load()
-    lib.ssnt_fused_decode_select.restype = ctypes.c_int
-    assert lib.ssnt_fused_decode_select(request.param) == 0
-    yield request.param
-    lib.ssnt_fused_decode_select(-1)
+    """The fused decodes' two step orderings (full rank: the product; selection: forced through
+    the A/B build, include/ssnt_tts_c_ab.h) must give identical outputs."""
+    if request.param == 0:
+        yield 0
+        return
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_fused_decode_select(1) == 0
+        yield 1
 
 
 def _same(g, o, keys, ctx):

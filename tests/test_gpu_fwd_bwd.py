@@ -17,11 +17,16 @@ F_TERM, F_ZINF = 1, 2
 
 @pytest.fixture(autouse=True, params=[0, 1, 2], ids=["default", "simple", "segmented"])
 def kernel_variant(request, gpu):
-    """Every parity case runs on every kernel (they must be bit-identical)."""
-    lib = gpu.load()
-    assert lib.ssnt_fwd_bwd_set_variant(request.param) == 0
-    yield request.param
-    lib.ssnt_fwd_bwd_set_variant(0)
+    """Every parity case runs on every kernel (they must be bit-identical): the product library's
+    own dispatch, and the two-wave / segmented kernels forced through the A/B build
+    (include/ssnt_tts_c_ab.h)."""
+    if request.param == 0:
+        yield 0
+        return
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_fwd_bwd_set_variant(request.param) == 0
+        yield request.param
+        ab.ssnt_fwd_bwd_set_variant(0)
 
 
 def _run_gpu(gpu, lt, S, P, lo=None, flags=F_TERM, debug=True):
@@ -90,6 +95,48 @@ def test_bit_exact_ragged_and_edges(gpu, oracle, seed, flags):
     _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
 
 
+ROWS_SHAPES = [  # (B, T, U): the rows kernel's K = 1 / K = 2 layouts and its three ring depths
+    (40, 48, 33),    # K=1, R=24: every S = 1..40 (both parities of S and of the cut)
+    (40, 48, 80),    # K=2, R=24
+    (12, 200, 128),  # K=2 at the LDS edge: R=8, NB=2
+    (9, 30, 64),     # K=1 upper edge
+    (9, 30, 66),     # K=2 lower edge
+]
+
+
+@pytest.mark.parametrize("shape", ROWS_SHAPES)
+@pytest.mark.parametrize("flags", [F_TERM, 0])
+def test_rows_kernel_every_length(gpu, oracle, shape, flags):
+    # The rows kernel (fwd_bwd_rows.hip) keeps only even lattice rows and rebuilds the odd ones in
+    # its gradient pairs; the cut M = (S-1)>>1 and the pairs (2j, 2j+1) meet differently for
+    # every S, so sweep S = 1.. with P from 1 to S (one path), ragged, plus infeasible S < P.
+    B, T, U = shape
+    rng = np.random.default_rng(B * T + U)
+    S = np.array([min(i + 1, T) for i in range(B)]) if B < 20 else np.arange(1, B + 1)
+    if T >= 100:  # long lattices: every cut parity near the full length too
+        S = np.array([T - i for i in range(B)])
+    P = np.array([int(rng.integers(1, min(s, U) + 1)) for s in S])
+    P[::5] = np.minimum(S[::5], U)  # S == P where U allows: the single path
+    if S[3] < U:
+        P[3] = S[3] + 1  # infeasible (S < P)
+    lt = oracle.synth_log_trans(B, T, U, seed=U + T)
+    g = _run_gpu(gpu, lt, S, P, flags=flags)
+    o = oracle.fwd_bwd_xf(lt, S, P, flags=flags, debug=True)
+    _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+
+
+def test_rows_kernel_is_the_default_at_config2(gpu, kernel_variant):
+    # the product's dispatch runs the rows kernel at BASELINE configs[1] (and configs[0], [3])
+    if kernel_variant != 0:
+        pytest.skip("the product's own dispatch")
+    dev = torch.device("cuda:0")
+    for (B, T, U) in [(2, 200, 80), (1, 50, 20)]:
+        x = torch.zeros((B, T, U, 2), device=dev)
+        gpu.ssnt_fwd_bwd(x, torch.full((B,), T, dtype=torch.int32, device=dev),
+                         torch.full((B,), U, dtype=torch.int32, device=dev), check=True)
+        assert gpu.last_fwd_bwd_kernel().startswith("k_fwd_bwd_rows<"), gpu.last_fwd_bwd_kernel()
+
+
 def test_workspace_mode_long_rows(gpu, oracle):
     # T*U*8 bytes > LDS budget -> rows live in the global workspace
     B, T, U = 3, 320, 80
@@ -131,16 +178,13 @@ def wide_lanes(request, gpu):
     """The long-row kernel's two lane widths (positions per lane), each with a direction's
     segments split over two workgroups (global hand-off) and in one workgroup, must be
     bit-identical."""
-    import ctypes
-    lib = gpu.load()
-    lib.ssnt_fwd_bwd_wide_lanes.restype = ctypes.c_int
-    lib.ssnt_fwd_bwd_wide_split.restype = ctypes.c_int
     k, split = request.param
-    assert lib.ssnt_fwd_bwd_wide_lanes(k) == 0
-    assert lib.ssnt_fwd_bwd_wide_split(split) == 0
-    yield k
-    lib.ssnt_fwd_bwd_wide_lanes(1)
-    lib.ssnt_fwd_bwd_wide_split(-1)
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_fwd_bwd_wide_lanes(k) == 0
+        assert ab.ssnt_fwd_bwd_wide_split(split) == 0
+        yield k
+        ab.ssnt_fwd_bwd_wide_lanes(1)
+        ab.ssnt_fwd_bwd_wide_split(-1)
 
 
 WIDE_SHAPES = [  # the long-row kernel (256 < U <= 512): 3..8 waves per direction, odd U
@@ -210,11 +254,8 @@ def test_tuning_wave_mixes_bit_exact(gpu, oracle, kernel_variant, variant):
     # K = 2 shapes) must be bit-identical to the oracle like the default mix
     if kernel_variant != 0:
         pytest.skip("mix variants are streaming-kernel variants")
-    lib = gpu.load()
-    rc = lib.ssnt_fwd_bwd_set_variant(variant)
-    if rc == 5:  # SSNT_ERR_UNSUPPORTED: the tuning mixes exist in `make lib-exp` builds only
-        pytest.skip("tuning mixes are compiled out of the product library")
-    assert rc == 0
+    if gpu.load_ab().ssnt_fwd_bwd_set_variant(variant) == 5:  # SSNT_ERR_UNSUPPORTED
+        pytest.skip("tuning mixes exist in the `make lib-exp` build only")
     rng = np.random.default_rng(variant)
     B, T, U = 6, 90, 80
     P = rng.integers(1, U + 1, size=B)
@@ -453,11 +494,8 @@ def test_stream_ring_depth_variants(gpu, oracle, kernel_variant, ring):
     # must be bit-identical to the oracle (ragged batch, debug rows)
     if kernel_variant != 0:
         pytest.skip("a streaming-kernel form")
-    import ctypes
-    lib = gpu.load()
-    lib.ssnt_fwd_bwd_stream_ring.restype = ctypes.c_int
-    assert lib.ssnt_fwd_bwd_stream_ring(ring) == 0
-    try:
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_fwd_bwd_stream_ring(ring) == 0
         rng = np.random.default_rng(ring)
         B, T, U = 6, 200, 80
         lt = oracle.synth_log_trans(B, T, U, seed=ring)
@@ -467,5 +505,3 @@ def test_stream_ring_depth_variants(gpu, oracle, kernel_variant, ring):
         assert f"RS={ring}" in gpu.last_fwd_bwd_kernel() and "LDS=0" in gpu.last_fwd_bwd_kernel()
         o = oracle.fwd_bwd_xf(lt, S, P, debug=True)
         _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
-    finally:
-        lib.ssnt_fwd_bwd_stream_ring(0)

@@ -18,12 +18,11 @@ F_TERM, F_ZINF = 1, 2
 
 @pytest.fixture(autouse=True)
 def pair_variant(gpu):
-    """The pair kernel is selected with ssnt_fwd_bwd_set_variant(12) (the default dispatch keeps
+    """The pair kernel is selected with the A/B build's ssnt_fwd_bwd_set_variant(12) (the product keeps
     the one-step streaming kernel, which measured faster: DESIGN.md 5.1a)."""
-    lib = gpu.load()
-    assert lib.ssnt_fwd_bwd_set_variant(12) == 0
-    yield
-    lib.ssnt_fwd_bwd_set_variant(0)
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_fwd_bwd_set_variant(12) == 0
+        yield
 
 
 def _run(gpu, lt, S, P, flags=F_TERM, debug=True, shift=0):

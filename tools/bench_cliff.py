@@ -26,9 +26,15 @@ def case(B, T, U, shift, variant):
     if T < U:
         raise ValueError(f"infeasible timing shape B={B} T={T} U={U}: every utterance has S < P, "
                          "so the kernel would only zero-fill grad")
-    lib = S.load()
-    if lib.ssnt_fwd_bwd_set_variant(variant) != 0:
-        return None
+    if variant:  # the two-wave kernel forced through the A/B build (include/ssnt_tts_c_ab.h)
+        with S.use_ab() as ab:
+            if ab.ssnt_fwd_bwd_set_variant(variant) != 0:
+                return None
+            return _case(B, T, U, shift, variant)
+    return _case(B, T, U, shift, variant)
+
+
+def _case(B, T, U, shift, variant):
     lt = O.synth_log_trans(B, T, U, seed=0)
     flat = torch.zeros(lt.size + shift, dtype=torch.float32, device=DEV)
     flat[shift:] = torch.from_numpy(lt.ravel()).to(DEV)
@@ -56,4 +62,3 @@ if __name__ == "__main__":
             r = case(B, T, U, shift, v)
             if r:
                 print(json.dumps(r), flush=True)
-    S.load().ssnt_fwd_bwd_set_variant(0)

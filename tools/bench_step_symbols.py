@@ -60,10 +60,6 @@ def raw_v1(lib, c, n=5000):
     g = ol.oracle_v1_step
     out = {"raw_gpu_v1_W4_us": per_call(lambda: f(*gargs), n=n),
            "raw_cpu_v1_W4_us": per_call(lambda: g(*oargs), n=n)}
-    lib.ssnt_diag_step_clock.restype = ctypes.c_int
-    lib.ssnt_diag_step_clock.argtypes = [ctypes.c_int, vp]
-    lib.ssnt_diag_null_launch.restype = ctypes.c_int
-    lib.ssnt_diag_null_launch.argtypes = [ctypes.c_int, vp]
     ph = np.zeros(5)
     lib.ssnt_diag_step_clock(1, None)
     for _ in range(n):
@@ -79,9 +75,11 @@ def raw_v1(lib, c, n=5000):
 
 
 def main():
-    lib = _lib.load()
-    lib.ssnt_set_host_staging.restype = ctypes.c_int
-    lib.ssnt_set_host_staging.argtypes = [ctypes.c_int]
+    with _lib.use_ab() as lib:  # the host staging / sync knobs are A/B-build symbols
+        _main(lib)
+
+
+def _main(lib):
     empty = per_call(lambda: lib.ssnt_status_from_bits(0), n=20000)
     res = {"empty_ctypes_call_us": empty}
     # v1 step, W=4, batch 1 (the reference symbol's fixed batch, ssnt_tts_c/src/lib.rs:13)
@@ -106,8 +104,6 @@ def main():
                           c2["u"], c2["input_length"], np.zeros(64, np.int32), 0, False, True),
         n=500)
     res.update(raw_v1(lib, c))
-    lib.ssnt_set_host_sync.restype = ctypes.c_int
-    lib.ssnt_set_host_sync.argtypes = [ctypes.c_int]
     prev = lib.ssnt_set_host_sync(0)
     for mode in (0, 1, 2):  # completion: hipStreamSynchronize / hipStreamWriteValue32 / flag kernel
         lib.ssnt_set_host_sync(mode)

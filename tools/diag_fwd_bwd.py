@@ -15,7 +15,8 @@ import torch  # noqa: E402
 import ssnt_tts_amd as S  # noqa: E402
 
 VARIANT = int(os.environ.get("SSNT_VARIANT", "0"))  # 0 default mix, 2..6 tuning mixes
-NC, NH = {0: (3, 4), 2: (4, 2), 3: (3, 2), 4: (2, 4), 5: (2, 2), 6: (2, 3), 7: (3, 3), 8: (3, 4)}[VARIANT]
+NC, NH = {0: (3, 4), 2: (4, 2), 3: (3, 2), 4: (2, 4), 5: (2, 2), 6: (2, 3), 7: (3, 3), 8: (3, 4),
+          13: (3, 4)}[VARIANT]  # 0: the rows kernel (default), 13: the streaming kernel
 ROLES = ["alpha chain", "beta chain"] + [f"conv {'fb'[i % 2]}{i // 2}" for i in range(2 * NC)] + \
         [f"grad {'fb'[i % 2]}{i // 2}" for i in range(2 * NH)]
 B, T, U = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (256, 200, 80)))
@@ -34,7 +35,7 @@ buf = np.zeros((1024, 18, 8), np.uint64)
 n = lib.ssnt_diag_read(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes)
 assert n > 0, "not a diagnostic build"
 d = buf[:min(B, 1024)].astype(np.float64)
-print(f"B={B} T={T} U={U}: median over utterances (cycles)")
+print(f"B={B} T={T} U={U} kernel {S.last_fwd_bwd_kernel()}: median over utterances (cycles)")
 times = []
 for _ in range(5):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
