@@ -329,7 +329,8 @@ int launch_simple(const FwdBwdArgs& a, hipStream_t st) {
 // tests and tools only) adds a process-wide override: 1 two-wave kernel only, 2 segmented
 // kernel, 3 the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs; its own rounding
 // order, oracle ORACLE_PAIR; measured slower: DESIGN.md 5.1a), 4 the streaming kernel where the
-// rows kernel would run; SSNT_FWD_BWD_KERNEL=simple selects 1 there.
+// rows kernel would run, 5 the rows kernel with row-layout converters; SSNT_FWD_BWD_KERNEL=simple
+// selects 1 there.
 #ifdef SSNT_AB
 std::atomic<int> g_variant{0};
 std::once_flag g_variant_env;
@@ -385,13 +386,14 @@ int set_fwd_bwd_variant(int v) {
   // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel at every U it takes; 3..11
   // (SSNT_EXP builds only): streaming kernel with another wave mix / ring / publication period;
   // 12: the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs); 13: the streaming
-  // kernel where the rows kernel would run (fwd_bwd_stream.hip)
-  if (v < 0 || v > 13) return SSNT_ERR_INVALID_ARG;
+  // kernel where the rows kernel would run (fwd_bwd_stream.hip); 14: the rows kernel with its
+  // row-layout converters (K = 2; the default converts dense chunks)
+  if (v < 0 || v > 14) return SSNT_ERR_INVALID_ARG;
 #ifndef SSNT_EXP
   if (v >= 3 && v < 12) return SSNT_ERR_UNSUPPORTED;
 #endif
   variant();  // the environment is read once, before any explicit choice
-  g_variant.store(v == 12 ? 3 : v == 13 ? 4 : v >= 3 ? 0 : v);
+  g_variant.store(v == 12 ? 3 : v == 13 ? 4 : v == 14 ? 5 : v >= 3 ? 0 : v);
   set_stream_mix(v >= 3 && v < 12 ? v - 2 : 0);
   return SSNT_OK;
 }
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(64) void k_loss_sum(const float* loss, int B, float
 
 int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
   summed = false;
-  if (variant() == 0 || variant() == 3 || variant() == 4) {
+  if (variant() == 0 || variant() == 3 || variant() == 4 || variant() == 5) {
     FwdBwdArgs x = a;
 #ifdef SSNT_EXP
     const char* ee = getenv("SSNT_EXP");
@@ -416,7 +418,8 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
 #ifdef SSNT_AB
     if (variant() == 3 && stream_ring() == 0) rc = launch_fwd_bwd_pair(x, st);
 #endif
-    if (rc == SSNT_ERR_UNSUPPORTED && variant() == 0 && stream_ring() == 0) rc = launch_fwd_bwd_rows(x, st);
+    if (rc == SSNT_ERR_UNSUPPORTED && (variant() == 0 || variant() == 5) && stream_ring() == 0)
+      rc = launch_fwd_bwd_rows(x, st, variant() == 0);
     if (rc == SSNT_ERR_UNSUPPORTED) rc = launch_fwd_bwd_stream(x, st);
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;

@@ -43,6 +43,7 @@ constexpr int kRowsNC = 3, kRowsNH = 4;         // converters / gradient waves p
 constexpr int kRowsWaves = 2 + 2 * kRowsNC + 2 * kRowsNH;  // 16
 constexpr int kRowsR2 = 8;                     // chain-row ring rows per direction
 constexpr int kRowsConvDepth = 8;              // converter prefetch (rows of log_trans in flight)
+constexpr int kChunk = 8;                      // rows per dense-converter chunk (DC)
 
 // LDS: ctl | cutA, cutB (64K xf each) | junk (64 x 16K B) | factor rings |
 //      chain-row rings [2][kR2][U xf] | kept rows [(T+1)/2][U xf] (lattice row s at s >> 1)
@@ -104,7 +105,7 @@ __device__ __forceinline__ XRow<K> terminal_row(const XRow<K>& E, int p0, int P,
   return X;
 }
 
-template <int K, int R, int NB>
+template <int K, int R, int NB, bool DC>
 __global__ __launch_bounds__(64 * kRowsWaves) void k_fwd_bwd_rows(FwdBwdArgs a) {
   constexpr int kNC = kRowsNC, kNH = kRowsNH, kWaves = kRowsWaves, kR2 = kRowsR2;
   static_assert(NB % 2 == 0 && R % NB == 0 && (R / NB) % 2 == 0 && R % kR2 == 0 && R % 4 == 0 &&
@@ -187,7 +188,18 @@ __global__ __launch_bounds__(64 * kRowsWaves) void k_fwd_bwd_rows(FwdBwdArgs a) 
     for (int h = 0; h < kNH; ++h) m = max(m, jb0 - h - kNH * ctr_ld(&ctl->help[1][h]));
     return m;
   };
-  auto conv_rows = [&](int d) { return first_missing<kNC>(ctl->conv[d], 0); };
+  // rows converted (a prefix): converter c owns rows c, c + kNC, ... -- or, dense (DC), chunks
+  // of kChunk rows c, c + kNC, ...; conv[d][c] counts its rows / chunks done
+  auto conv_rows = [&](int d) {
+    if constexpr (DC) {
+      int m = INT_MAX;
+#pragma unroll
+      for (int c = 0; c < kNC; ++c) m = min(m, kChunk * (c + kNC * ctr_ld(&ctl->conv[d][c])));
+      return m;
+    } else {
+      return first_missing<kNC>(ctl->conv[d], 0);
+    }
+  };
   // factor entry of stream row r, lane l, element block 0 (block q: + q * nl * kEnt)
   auto slot_l = [&](int d, int r, int l) { return inr + ((size_t)(d * K) * nl + l) * kEnt + 16 * (r % R); };
   auto slot = [&](int d, int r) { return slot_l(d, r, pr / K); };
@@ -390,6 +402,116 @@ __global__ __launch_bounds__(64 * kRowsWaves) void k_fwd_bwd_rows(FwdBwdArgs a) 
       }
     }
     dg.flush(b, role.slot);
+    return;
+  }
+
+  if (DC && role.kind == 1) {
+    // ============================ dense converters (K = 2) ===============================
+    // A chunk = kChunk consecutive stream rows, contiguous in log_trans; its nl = U/2 position
+    // pairs per row are spread over all 64 lanes: item t of chunk k is granule g = 64 t + lane,
+    // row rr = g / nl of the chunk, pair l = g % nl (NI = ceil(kChunk nl / 64) items; at U = 80
+    // 5 items for 8 rows, where the row layout spends 8 wave-passes with 24 idle lanes each).
+    // The loads are 1 KiB contiguous per wave-instruction; the forward ring's pre-shift
+    // L[2l] = Sh[2l-1] comes from the lane before (DPP), lane 0 from the previous item's lane 63.
+    const int d = role.d;
+    const int c = role.idx;
+    constexpr int D = kRowsConvDepth;  // items in flight
+    const unsigned tag0 = (d == 0 && c == 0 && b == 0 && a.loss_sum) ? sum_tag(a) : 0u;
+    const int NI = (kChunk * nl + 63) >> 6;
+    const int nchunks = (S + kChunk - 1) / kChunk;
+    const int mine = nchunks > c ? (nchunks - c + kNC - 1) / kNC : 0;  // chunks c, c + kNC, ...
+    const int nitems = mine * NI;
+    const unsigned mnl = ((1u << 20) + (unsigned)nl - 1) / (unsigned)nl;  // g / nl = g * mnl >> 20
+    const __amdgpu_buffer_rsrc_t lt_r = brsrc(lt, (unsigned)(TU * 8));
+    auto item_src = [&](int t) {  // byte offset of item t's granule (negative: before the tensor)
+      const int k = t / NI, it = t - k * NI;
+      const int cc = c + kNC * k;
+      const int g = 64 * it + lane;
+      const int row0 = d == 0 ? kChunk * cc : S - kChunk - kChunk * cc;  // lowest lattice row
+      return (row0 * nl + g) * 16;
+    };
+    auto load = [&](int t, float* v) {
+      const int off = item_src(t);
+      buf_ld<4>(v, lt_r, off >= 0 ? off : INT_MIN);  // (out of range: zeros)
+    };
+    float pf[D][4];
+#pragma unroll
+    for (int i = 0; i < D; ++i) load(i, pf[i]);
+    int seen_read = 0;
+    int fwd_nd = d == 0 ? jf0 : 0, bwd_nd = d == 1 ? jb0 : 0;
+    const int grow0 = d == 0 ? M : S - M;
+    float carry_m = 0.0f;  // Sh[2l+1] of the previous item's lane 63 (forward pre-shift)
+    int carry_e = XF_EZERO;
+    for (int base = 0; base < nitems; base += D) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const int t = base + i;
+        if (t < nitems) {
+          const int k = t / NI, it = t - k * NI;
+          const int cc = c + kNC * k;  // chunk: stream rows kChunk cc .. + kChunk - 1
+          if (it == 0) {
+            // the chunk's slots last held stream rows up to kChunk (cc + 1) - 1 - R: read by the
+            // chain, and (gradient rows of this direction) by a gradient pair
+            const int qmax = kChunk * (cc + 1) - 1 - R;
+            if (qmax >= 0) {
+              if (seen_read <= qmax)
+                seen_read = spin_until<true>([&] { return ctr_ld(&ctl->sread[d]); }, qmax + 1, a.status, dg);
+              if (qmax >= grow0) {
+                if (d == 0) {
+                  const int pj = qmax >> 1;
+                  if (fwd_nd <= pj)
+                    fwd_nd = spin_until<true>([&] { return fwd_not_done(); }, pj + 1, a.status, dg);
+                } else {
+                  const int pj = (S - 1 - qmax) >> 1;
+                  if (bwd_nd >= pj)
+                    bwd_nd = -spin_until<true>([&] { return -bwd_not_done(); }, 1 - pj, a.status, dg);
+                }
+              }
+            }
+            carry_m = 0.0f;
+            carry_e = XF_EZERO;
+          }
+          const int g = 64 * it + lane;
+          const int rl = (int)(((unsigned)g * mnl) >> 20);  // row of the chunk, in lattice order
+          const int l = g - rl * nl;
+          const int rr = d == 0 ? rl : kChunk - 1 - rl;  // row of the chunk, in stream order
+          const int r = kChunk * cc + rr;                // stream row
+          const bool live = rl < kChunk && r < S;
+          const int pp = 2 * l;
+          float em0, ms0, em1, ms1;
+          int ee0, es0, ee1, es1;
+          xf_exp_pair(pf[i][0], pf[i][1], pp < P, pp < P - 1, em0, ee0, ms0, es0);
+          xf_exp_pair(pf[i][2], pf[i][3], pp + 1 < P, pp + 1 < P - 1, em1, ee1, ms1, es1);
+          float xm0 = ms0, xm1 = ms1;
+          int xe0 = es0, xe1 = es1;
+          if (d == 0) {  // L[2l] = Sh[2l-1] (lane before; zero at l = 0), L[2l+1] = Sh[2l]
+            const float lm = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                 __builtin_bit_cast(int, carry_m), __builtin_bit_cast(int, ms1), 0x138, 0xf, 0xf, false));
+            const int le = __builtin_amdgcn_update_dpp(carry_e, es1, 0x138, 0xf, 0xf, false);
+            carry_m = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms1), 63));
+            carry_e = __builtin_amdgcn_readlane(es1, 63);
+            xm1 = ms0;
+            xe1 = es0;
+            xm0 = l == 0 ? 0.0f : lm;
+            xe0 = l == 0 ? XF_EZERO : le;
+          }
+          cbar();
+          if (live) {
+            unsigned char* e0 = slot_l(d, r, l);
+            const float v0[4] = {em0, __builtin_bit_cast(float, ee0), xm0, __builtin_bit_cast(float, xe0)};
+            const float v1[4] = {em1, __builtin_bit_cast(float, ee1), xm1, __builtin_bit_cast(float, xe1)};
+            st_vec<4>(reinterpret_cast<float*>(e0), v0);
+            st_vec<4>(reinterpret_cast<float*>(e0 + (size_t)nl * kEnt), v1);
+          }
+          cbar();
+          if (it == NI - 1) ctr_st(&ctl->conv[d][c], k + 1);
+        }
+        load(t + D, pf[i]);  // refill in place
+      }
+    }
+    dg.flush(b, role.slot);
+    fill_rows(S, d * kNC + c, 2 * kNC);  // zero the rows beyond S
+    if (d == 0 && c == 0 && b == 0 && a.loss_sum) finish_loss_sum(a, tag0);
     return;
   }
 
@@ -683,11 +805,11 @@ __global__ __launch_bounds__(64 * kRowsWaves) void k_fwd_bwd_rows(FwdBwdArgs a) 
   dg.flush(b, role.slot);
 }
 
-template <int K, int R, int NB>
+template <int K, int R, int NB, bool DC>
 int launch_rows_kernel(const FwdBwdArgs& a, hipStream_t st) {
-  auto kern = k_fwd_bwd_rows<K, R, NB>;
+  auto kern = k_fwd_bwd_rows<K, R, NB, DC>;
   const size_t lds = rows_lds_bytes(K, a.T, a.U, R);
-  note_fwd_bwd_dispatch("k_fwd_bwd_rows<K=%d,R=%d,NB=%d>", K, R, NB);
+  note_fwd_bwd_dispatch("k_fwd_bwd_rows<K=%d,R=%d,NB=%d,DC=%d>", K, R, NB, (int)DC);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
@@ -695,11 +817,11 @@ int launch_rows_kernel(const FwdBwdArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
-template <int K>
+template <int K, bool DC>
 int launch_rows_k(const FwdBwdArgs& a, hipStream_t st) {
-  if (rows_lds_bytes(K, a.T, a.U, 24) <= kLdsBudget) return launch_rows_kernel<K, 24, 4>(a, st);
-  if (rows_lds_bytes(K, a.T, a.U, 16) <= kLdsBudget) return launch_rows_kernel<K, 16, 4>(a, st);
-  if (rows_lds_bytes(K, a.T, a.U, 8) <= kLdsBudget) return launch_rows_kernel<K, 8, 2>(a, st);
+  if (rows_lds_bytes(K, a.T, a.U, 24) <= kLdsBudget) return launch_rows_kernel<K, 24, 4, DC>(a, st);
+  if (rows_lds_bytes(K, a.T, a.U, 16) <= kLdsBudget) return launch_rows_kernel<K, 16, 4, DC>(a, st);
+  if (rows_lds_bytes(K, a.T, a.U, 8) <= kLdsBudget) return launch_rows_kernel<K, 8, 2, DC>(a, st);
   return SSNT_ERR_UNSUPPORTED;
 }
 
@@ -707,14 +829,15 @@ inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 
 }  // namespace
 
-int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t st) {
+int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t st, bool dense) {
   // U <= 128 without log_obs, whole lane slices and 16-byte aligned tensors; else the streaming
   // kernel (which takes log_obs, odd U and 4- / 8-byte alignment)
   if (a.log_obs || a.U > 128) return SSNT_ERR_UNSUPPORTED;
   const int K = a.U <= 64 ? 1 : 2;
   if (a.U % K != 0 || !al16(a.log_trans) || !al16(a.grad) || !al16(a.log_alpha) || !al16(a.log_beta))
     return SSNT_ERR_UNSUPPORTED;
-  return K == 1 ? launch_rows_k<1>(a, st) : launch_rows_k<2>(a, st);
+  if (K == 1) return launch_rows_k<1, false>(a, st);
+  return dense ? launch_rows_k<2, true>(a, st) : launch_rows_k<2, false>(a, st);
 }
 
 size_t rows_kernel_lds(int T, int U) {  // 0 when the kernel does not take the shape

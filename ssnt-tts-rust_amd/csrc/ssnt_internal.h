@@ -42,7 +42,7 @@ size_t fwd_bwd_sum_state_bytes(int B);  // 64 + 8 B
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
 // rows kernel (fwd_bwd_rows.hip; the default for U <= 128 without log_obs, U % K == 0, 16-byte
 // aligned tensors, rows within LDS): SSNT_ERR_UNSUPPORTED for shapes it does not take
-int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t stream);
+int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t stream, bool dense = true);
 // streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t stream);
 void set_stream_mix(int m);  // tuning only (SSNT_EXP builds)
