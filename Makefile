@@ -14,11 +14,11 @@ ORACLE    := oracle/build/libssnt_oracle.so
 # the CPU oracle reproduces it bit for bit. Correctly rounded f32 division is HIP's default.
 HIPFLAGS  := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden -Wall \
              -Wno-unused-function -I include -I $(CSRC)
-HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/fwd_bwd_rows.hip $(CSRC)/fwd_bwd_stream.hip $(CSRC)/fwd_bwd_wide.hip $(CSRC)/v2_fwd_bwd.hip \
+HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/fwd_bwd_stream.hip $(CSRC)/fwd_bwd_wide.hip $(CSRC)/v2_fwd_bwd.hip \
              $(CSRC)/decode.hip \
              $(CSRC)/fused_decode.hip $(CSRC)/capi.hip
 # the A/B build adds the kernels only its knobs reach (the pair kernel)
-AB_SRCS   := $(HIP_SRCS) $(CSRC)/fwd_bwd_pair.hip
+AB_SRCS   := $(HIP_SRCS) $(CSRC)/fwd_bwd_pair.hip $(CSRC)/fwd_bwd_rows.hip
 HIP_HDRS  := $(wildcard $(CSRC)/*.h) include/ssnt_tts_c.h
 HIP_OBJS  := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(HIP_SRCS))
 

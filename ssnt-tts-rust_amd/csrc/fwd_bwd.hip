@@ -324,13 +324,13 @@ int launch_simple(const FwdBwdArgs& a, hipStream_t st) {
   return SSNT_ERR_UNSUPPORTED;
 }
 
-// Kernel choice. The product dispatches by shape only (rows kernel, else the streaming kernel,
-// else the segmented kernel, else the two-wave kernel). The A/B build (-DSSNT_AB, `make lib-ab`;
-// tests and tools only) adds a process-wide override: 1 two-wave kernel only, 2 segmented
-// kernel, 3 the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs; its own rounding
-// order, oracle ORACLE_PAIR; measured slower: DESIGN.md 5.1a), 4 the streaming kernel where the
-// rows kernel would run, 5 the rows kernel with row-layout converters; SSNT_FWD_BWD_KERNEL=simple
-// selects 1 there.
+// Kernel choice. The product dispatches by shape only (the streaming kernel, else the segmented
+// kernel, else the two-wave kernel). The A/B build (-DSSNT_AB, `make lib-ab`; tests and tools
+// only) adds a process-wide override: 1 two-wave kernel only, 2 segmented kernel, 3 the pair
+// kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs; its own rounding order, oracle
+// ORACLE_PAIR; measured slower: DESIGN.md 5.1a), 4 / 5 the rows kernel first (fwd_bwd_rows.hip,
+// dense / row-layout converters; bit-exact, measured slower: DESIGN.md 5.1c);
+// SSNT_FWD_BWD_KERNEL=simple selects 1 there.
 #ifdef SSNT_AB
 std::atomic<int> g_variant{0};
 std::once_flag g_variant_env;
@@ -385,9 +385,8 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
 int set_fwd_bwd_variant(int v) {
   // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel at every U it takes; 3..11
   // (SSNT_EXP builds only): streaming kernel with another wave mix / ring / publication period;
-  // 12: the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs); 13: the streaming
-  // kernel where the rows kernel would run (fwd_bwd_stream.hip); 14: the rows kernel with its
-  // row-layout converters (K = 2; the default converts dense chunks)
+  // 12: the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs); 13 / 14: the rows
+  // kernel first (fwd_bwd_rows.hip, U <= 128 without log_obs; dense / row-layout converters)
   if (v < 0 || v > 14) return SSNT_ERR_INVALID_ARG;
 #ifndef SSNT_EXP
   if (v >= 3 && v < 12) return SSNT_ERR_UNSUPPORTED;
@@ -417,9 +416,8 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
     int rc = SSNT_ERR_UNSUPPORTED;
 #ifdef SSNT_AB
     if (variant() == 3 && stream_ring() == 0) rc = launch_fwd_bwd_pair(x, st);
+    if ((variant() == 4 || variant() == 5) && stream_ring() == 0) rc = launch_fwd_bwd_rows(x, st, variant() == 4);
 #endif
-    if (rc == SSNT_ERR_UNSUPPORTED && (variant() == 0 || variant() == 5) && stream_ring() == 0)
-      rc = launch_fwd_bwd_rows(x, st, variant() == 0);
     if (rc == SSNT_ERR_UNSUPPORTED) rc = launch_fwd_bwd_stream(x, st);
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;

@@ -1,5 +1,6 @@
-// fwd_bwd_rows.hip -- the default lattice forward-backward for U <= 128 without log_obs
-// (gfx950): batch-fed chains, half the lattice rows kept, the other half rebuilt on demand.
+// fwd_bwd_rows.hip -- an A/B lattice forward-backward for U <= 128 without log_obs (gfx950;
+// `make lib-ab` variants 13 / 14 only: bit-exact, measured slower than the streaming kernel,
+// DESIGN.md 5.1c): batch-fed chains, half the lattice rows kept, the other half rebuilt on demand.
 //
 // Same lattice and the same split-exponent arithmetic as every fwd-bwd kernel,
 // bit-exact with oracle/ssnt_oracle.c. One workgroup = one utterance, 16 waves in the roles of
@@ -43,7 +44,12 @@ constexpr int kRowsNC = 3, kRowsNH = 4;         // converters / gradient waves p
 constexpr int kRowsWaves = 2 + 2 * kRowsNC + 2 * kRowsNH;  // 16
 constexpr int kRowsR2 = 8;                     // chain-row ring rows per direction
 constexpr int kRowsConvDepth = 8;              // converter prefetch (rows of log_trans in flight)
-constexpr int kChunk = 8;                      // rows per dense-converter chunk (DC)
+// rows per dense-converter chunk (DC). A converter overwrites a chunk's slots only when the
+// chain has read the chunk R rows before it and the gradient pairs of those rows are done; the
+// chain asks for rows 2 NB ahead of what it has written, so a chunk must fit in R - 2 NB + 1 rows
+// or the converter would wait on alpha / beta rows the chain cannot produce yet (a deadlock).
+template <int R, int NB>
+constexpr int rows_chunk() { return R - 2 * NB + 1 >= 8 ? 8 : 4; }
 
 // LDS: ctl | cutA, cutB (64K xf each) | junk (64 x 16K B) | factor rings |
 //      chain-row rings [2][kR2][U xf] | kept rows [(T+1)/2][U xf] (lattice row s at s >> 1)
@@ -108,6 +114,8 @@ __device__ __forceinline__ XRow<K> terminal_row(const XRow<K>& E, int p0, int P,
 template <int K, int R, int NB, bool DC>
 __global__ __launch_bounds__(64 * kRowsWaves) void k_fwd_bwd_rows(FwdBwdArgs a) {
   constexpr int kNC = kRowsNC, kNH = kRowsNH, kWaves = kRowsWaves, kR2 = kRowsR2;
+  constexpr int kChunk = rows_chunk<R, NB>();
+  static_assert(R >= 2 * NB + kChunk - 1, "a dense-converter chunk must fit behind the chain");
   static_assert(NB % 2 == 0 && R % NB == 0 && (R / NB) % 2 == 0 && R % kR2 == 0 && R % 4 == 0 &&
                 R >= 2 * NB && kR2 > NB, "batch / ring sizes");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -40,9 +40,6 @@ struct FwdBwdArgs {
 size_t fwd_bwd_workspace_bytes(int B, int T, int U);
 size_t fwd_bwd_sum_state_bytes(int B);  // 64 + 8 B
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
-// rows kernel (fwd_bwd_rows.hip; the default for U <= 128 without log_obs, U % K == 0, 16-byte
-// aligned tensors, rows within LDS): SSNT_ERR_UNSUPPORTED for shapes it does not take
-int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t stream, bool dense = true);
 // streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t stream);
 void set_stream_mix(int m);  // tuning only (SSNT_EXP builds)
@@ -63,6 +60,9 @@ int set_fwd_bwd_wide_split(int mode);  // two workgroups per direction (-1 auto,
 int launch_fwd_bwd_pair(const FwdBwdArgs& a, hipStream_t stream);
 size_t pair_head_bytes(int K, int U);            // LDS bytes besides the stored rows
 size_t pair_storage_bytes(int K, int T, int U);  // stored rows of one utterance
+// rows kernel (fwd_bwd_rows.hip; U <= 128 without log_obs, U % K == 0, 16-byte aligned tensors,
+// rows within LDS): SSNT_ERR_UNSUPPORTED for shapes it does not take
+int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t stream, bool dense = true);
 int set_fused_decode_select(int mode);  // -1 default, 0 full rank, 1 selection
 #else
 constexpr int stream_ring() { return 0; }

@@ -15,11 +15,12 @@ pytestmark = pytest.mark.gpu
 F_TERM, F_ZINF = 1, 2
 
 
-@pytest.fixture(autouse=True, params=[0, 1, 2], ids=["default", "simple", "segmented"])
+@pytest.fixture(autouse=True, params=[0, 1, 2, 13], ids=["default", "simple", "segmented", "rows"])
 def kernel_variant(request, gpu):
     """Every parity case runs on every kernel (they must be bit-identical): the product library's
-    own dispatch, and the two-wave / segmented kernels forced through the A/B build
-    (include/ssnt_tts_c_ab.h)."""
+    own dispatch, and the two-wave / segmented / rows kernels forced through the A/B build
+    (include/ssnt_tts_c_ab.h; the rows kernel declines log_obs and U > 128, which then take the
+    product's dispatch)."""
     if request.param == 0:
         yield 0
         return
@@ -106,10 +107,15 @@ ROWS_SHAPES = [  # (B, T, U): the rows kernel's K = 1 / K = 2 layouts and its th
 
 @pytest.mark.parametrize("shape", ROWS_SHAPES)
 @pytest.mark.parametrize("flags", [F_TERM, 0])
-def test_rows_kernel_every_length(gpu, oracle, shape, flags):
-    # The rows kernel (fwd_bwd_rows.hip) keeps only even lattice rows and rebuilds the odd ones in
-    # its gradient pairs; the cut M = (S-1)>>1 and the pairs (2j, 2j+1) meet differently for
-    # every S, so sweep S = 1.. with P from 1 to S (one path), ragged, plus infeasible S < P.
+@pytest.mark.parametrize("rows_variant", [13, 14], ids=["dense-conv", "row-conv"])
+def test_rows_kernel_every_length(gpu, oracle, kernel_variant, rows_variant, shape, flags):
+    # The rows kernel (fwd_bwd_rows.hip, A/B build) keeps only even lattice rows and rebuilds the
+    # odd ones in its gradient pairs; the cut M = (S-1)>>1 and the pairs (2j, 2j+1) meet
+    # differently for every S, so sweep S = 1.. with P from 1 to S (one path), ragged, plus
+    # infeasible S < P. Both converter forms; the deepest ring (R = 8) sets the dense converters'
+    # chunk (a chunk that does not fit behind the chain deadlocks: rows_chunk()).
+    if kernel_variant != 0:
+        pytest.skip("selects its own kernel")
     B, T, U = shape
     rng = np.random.default_rng(B * T + U)
     S = np.array([min(i + 1, T) for i in range(B)]) if B < 20 else np.arange(1, B + 1)
@@ -120,13 +126,17 @@ def test_rows_kernel_every_length(gpu, oracle, shape, flags):
     if S[3] < U:
         P[3] = S[3] + 1  # infeasible (S < P)
     lt = oracle.synth_log_trans(B, T, U, seed=U + T)
-    g = _run_gpu(gpu, lt, S, P, flags=flags)
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_fwd_bwd_set_variant(rows_variant) == 0
+        g = _run_gpu(gpu, lt, S, P, flags=flags)
+        assert gpu.last_fwd_bwd_kernel().startswith("k_fwd_bwd_rows<"), gpu.last_fwd_bwd_kernel()
     o = oracle.fwd_bwd_xf(lt, S, P, flags=flags, debug=True)
     _assert_bit_exact(g, o, ["loss", "grad", "log_alpha", "log_beta"])
 
 
-def test_rows_kernel_is_the_default_at_config2(gpu, kernel_variant):
-    # the product's dispatch runs the rows kernel at BASELINE configs[1] (and configs[0], [3])
+def test_streaming_kernel_is_the_default_at_config2(gpu, kernel_variant):
+    # the product's dispatch runs the streaming kernel at BASELINE configs[1] (and configs[0]);
+    # the product library carries no rows / pair kernel
     if kernel_variant != 0:
         pytest.skip("the product's own dispatch")
     dev = torch.device("cuda:0")
@@ -134,7 +144,7 @@ def test_rows_kernel_is_the_default_at_config2(gpu, kernel_variant):
         x = torch.zeros((B, T, U, 2), device=dev)
         gpu.ssnt_fwd_bwd(x, torch.full((B,), T, dtype=torch.int32, device=dev),
                          torch.full((B,), U, dtype=torch.int32, device=dev), check=True)
-        assert gpu.last_fwd_bwd_kernel().startswith("k_fwd_bwd_rows<"), gpu.last_fwd_bwd_kernel()
+        assert gpu.last_fwd_bwd_kernel().startswith("k_fwd_bwd_stream<"), gpu.last_fwd_bwd_kernel()
 
 
 def test_workspace_mode_long_rows(gpu, oracle):

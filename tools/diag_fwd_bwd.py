@@ -16,7 +16,7 @@ import ssnt_tts_amd as S  # noqa: E402
 
 VARIANT = int(os.environ.get("SSNT_VARIANT", "0"))  # 0 default mix, 2..6 tuning mixes
 NC, NH = {0: (3, 4), 2: (4, 2), 3: (3, 2), 4: (2, 4), 5: (2, 2), 6: (2, 3), 7: (3, 3), 8: (3, 4),
-          13: (3, 4), 14: (3, 4)}[VARIANT]  # 0: the rows kernel (default), 13: the streaming kernel
+          13: (3, 4), 14: (3, 4)}[VARIANT]  # 0: the streaming kernel (default), 13 / 14: the rows kernel
 ROLES = ["alpha chain", "beta chain"] + [f"conv {'fb'[i % 2]}{i // 2}" for i in range(2 * NC)] + \
         [f"grad {'fb'[i % 2]}{i // 2}" for i in range(2 * NH)]
 B, T, U = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (256, 200, 80)))
