@@ -10,21 +10,25 @@
 // State rows r = 0..I (input steps consumed) over totals x; only the window of row r
 // (f4_window: the v2 band, or [0, r*dmax] in test mode) can hold mass, so rows are stored
 // window-relative, Wcap xf wide:
-//   LDS:  duration table | class weights w[t] (2 steps) | 2 rows (ping-pong) | 2 chunks of
-//         staged class log-probs
+//   LDS:  duration table | class weights (xf, chunks of 64 steps, double-buffered) | 2 row
+//         buffers (ping-pong), each with kF4Pad zero cells on both sides of its window
 //   HBM:  alpha and beta rows 0..I of every utterance (workspace), Z per utterance.
 // A sweep step: each thread owns cells x = lo + tid (+512 ...) and sums its D class terms
 // (exponent max, then the ldexp-aligned f32 sum in class order; the class loop is unrolled for
-// D <= 64 with the durations in SGPRs); one barrier per step. Class log-probs are staged into
-// LDS a chunk of steps ahead (one global round trip per chunk) and converted one step before
-// use, so no global load sits on the I-step dependency chain. The forward workgroup also forms
-// Z (lane partials x mod 64 + butterfly) and the loss.
+// D <= 64, the step's weights read into registers once); one barrier per step. With the zero
+// cells around every window, a term's LDS address is one subtraction from its cell's (the
+// clamp to the window happens once per cell, not per term). Class log-probs are loaded a
+// chunk ahead and converted into LDS half a chunk later, so no global load and no exp sits on
+// the I-step dependency chain. The forward workgroup also forms Z (lane partials x mod 64 +
+// butterfly) and the loss.
 // Launch 2 (one workgroup per (utterance, step)): the gradients of step t -- class i on wave
 // i % 4, every class of a wave accumulated in one pass over the destination totals (lane
 // partial x mod 64, the oracle's order), one butterfly per class (DPP quad/mirror moves, a
 // swizzle, one bpermute) -- and the debug beta row. Fully parallel (B * I workgroups).
 #include <hip/hip_runtime.h>
+#include <limits.h>
 
+#include "buffer_ops.h"
 #include "ssnt_internal.h"
 #include "xf_math.h"
 
@@ -87,26 +91,35 @@ __device__ __forceinline__ void f4_log_row(float* dst, const xf* row, int lo, in
 // (source total x - d_i, product a.m * w.m); else beta (x + d_i, w.m * b.m). Classes padded to
 // DC = next power of two >= D with w = 0 and duration 0 (exact zero terms, as the oracle's
 // padding), so the 2 DC LDS reads of a cell issue back to back and the sum is the oracle's
-// pairwise tree (depth log2 DC instead of a DC-long add chain).
-template <bool FWD, int DC>
-__device__ __forceinline__ xf f4_cell(int x, const int* dur, const xf* w, const xf* src, int slo,
-                                      int span) {
-  // source window [slo, slo + span] (span = -1: empty). Offsets are taken +1, so everything left
-  // of the window is negative, i.e. huge unsigned, and one unsigned min clamps an out-of-window
-  // term onto the zero cell just right of the window (index span + 1), and offset 0 is the zero
-  // cell left of it (index -1): an exact zero term, as the oracle's skip
+// pairwise tree (depth log2 DC instead of a DC-long add chain). srcw is the source row's window
+// cell 0; every cell a term can reach outside the window holds the canonical zero (0, XF_EZERO):
+// an exact zero term, as the oracle's skip.
+//  PADDED (dmax <= kF4Pad): the row buffers carry kF4Pad zero cells on both sides of the window,
+//   and the caller clamps xr = x - slo into the band from which every term stays inside them, so
+//   a term's address is ONE subtraction from the cell's (8 d_i, hoisted out of the step loop).
+//  else: offsets are taken +1, so anything left of the window wraps to a huge unsigned value,
+//   and one unsigned min clamps an out-of-window term onto the zero cell just right of the window
+//   (index span + 1); offset 0 is the zero cell left of it (index -1).
+template <bool FWD, int DC, bool PADDED>
+__device__ __forceinline__ xf f4_cell(int xr, const int (&dk)[DC], const xf* w, const xf* srcw, int span) {
   float m[DC];
   int e[DC];
   int em = XF_EZERO;
-  int xr1 = x - slo + 1;
-  // opaque: otherwise the compiler reassociates xr1 - dur[i] into x + (1 - slo - dur[i]) with
-  // the 2 DC uniform sums in SGPRs, which overflows the SGPR file into lane spills every step
-  asm volatile("" : "+v"(xr1));
+  // opaque: otherwise the compiler reassociates the cell offset with the uniform durations into
+  // 2 DC uniform sums in SGPRs, which overflows the SGPR file into lane spills every step
+  int xb = PADDED ? xr : xr + 1;
+  asm volatile("" : "+v"(xb));
+  const xf* px = srcw + xb;  // PADDED: the cell's own source cell
   const unsigned lim = (unsigned)(span + 2);
 #pragma unroll
   for (int i = 0; i < DC; ++i) {
-    const unsigned yr1 = (unsigned)(FWD ? xr1 - dur[i] : xr1 + dur[i]);
-    const xf v = src[(int)min(yr1, lim) - 1];
+    xf v;
+    if constexpr (PADDED) {
+      v = px[FWD ? -dk[i] : dk[i]];
+    } else {
+      const unsigned yr1 = (unsigned)(FWD ? xb - dk[i] : xb + dk[i]);
+      v = srcw[(int)min(yr1, lim) - 1];
+    }
     const xf ww = w[i];
     m[i] = FWD ? v.m * ww.m : ww.m * v.m;
     e[i] = v.e + ww.e;
@@ -231,128 +244,198 @@ __device__ __forceinline__ F4Ws f4_ws(const V2FwdBwdArgs& a) {
   return F4Ws{base, base + rows, base + 2 * rows};
 }
 
+constexpr int kF4Pad = 64;  // zero cells either side of a row window (PADDED: dmax <= kF4Pad)
+// sweep steps per staged chunk of class weights
 template <int DC>
-__global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+constexpr int f4_chunk() { return DC <= 32 ? 64 : 32; }
+
+// One direction's sweep (FWD: alpha rows 0..I upward, and Z / the loss; else beta rows I..0).
+// LDS: durations | class weights [2][CH][DC] xf (a chunk of CH sweep steps, converted when staged)
+//      | row buffers [2][Wc + 2 kF4Pad + 2] xf (window cell j at kF4Pad + j; zeros around it)
+// A step: each thread owns cells x = lo + tid (+512 ...) of the new row and sums its DC class
+// terms from the previous row (f4_cell); one barrier per step. The class log-probs of chunk c + 1
+// are loaded into registers when chunk c starts and converted into LDS half a chunk later, so
+// no global load and no exp sits on the I-step dependency chain.
+template <int DC, bool FWD, bool PADDED>
+__device__ __forceinline__ void f4_sweep(const V2FwdBwdArgs& a, unsigned char* smem, const F4Utt& u,
+                                         int dmax) {
+  constexpr int CH = f4_chunk<DC>();
+  constexpr int NPF = (CH * DC + kF4Threads - 1) / kF4Threads;  // staged values per thread
   const int b = blockIdx.x;
-  const bool fwd = blockIdx.y == 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int D = a.D, X = a.X, Imax = a.Imax, Wc = a.Wcap;
-  constexpr int Dp = DC;  // class slots padded to DC (zero weight, duration 0)
-  int* dur = reinterpret_cast<int*>(smem);
-  xf* wbuf = reinterpret_cast<xf*>(smem + ((Dp * 4 + 15) & ~15));  // [2][Dp]
-  // row buffers [2][Wc + 3]: a zero cell, the window cells, a zero cell right after the window
-  // (rewritten every step), spare; rb(k) is buffer k's cell 0
-  xf* row = wbuf + 2 * Dp;
-  const int RS = Wc + 3;
-  auto rb = [&](int k) { return row + k * RS + 1; };
+  const int* dur = reinterpret_cast<const int*>(smem);
+  xf* cw = reinterpret_cast<xf*>(smem + ((DC * 4 + 15) & ~15));  // [2][CH][DC]
+  xf* row = cw + 2 * CH * DC;
+  const int RS = Wc + 2 * kF4Pad + 2;
+  auto rw = [&](int k) { return row + k * RS + kF4Pad; };  // buffer k's window cell 0
   const float* lg = a.logits + (size_t)b * Imax * D;
   const size_t drow = (size_t)(Imax + 1) * X;
-  float* la = a.log_alpha ? a.log_alpha + b * drow : nullptr;
+  float* la = (FWD && a.log_alpha) ? a.log_alpha + b * drow : nullptr;
   const F4Ws W = f4_ws(a);
-  xf* ws = (fwd ? W.alpha : W.beta) + (size_t)b * (Imax + 1) * Wc;
+  xf* ws = (FWD ? W.alpha : W.beta) + (size_t)b * (Imax + 1) * Wc;
   const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
-
-  for (int i = tid; i < Dp; i += kF4Threads) {
-    dur[i] = i < D ? a.table[i] : 0;
-    if (i >= D) wbuf[i] = wbuf[Dp + i] = xf_zero();
-  }
-  lds_sync();
-  F4Utt u;
-  if (!f4_setup(a, b, dur, u, fwd)) {
-    if (fwd) {
-      if (tid == 0) a.loss[b] = inf_loss;
-      if (la)
-        for (int r = 0; r <= Imax; ++r) f4_log_row(la + (size_t)r * X, nullptr, 0, -1, X);
-    }
-    return;
-  }
   const int I = u.I;
-  int dr[DC];  // durations in registers (VGPRs: the SGPR file is full with addresses)
+  int dk[DC];  // term offsets (VGPRs: the SGPR file is full with addresses)
 #pragma unroll
-  for (int i = 0; i < DC; ++i) dr[i] = dur[i];
-  auto cls_ok = [&](int i) { return a.allow_skip || i != a.zid; };
-  // class log-probs are staged through LDS in chunks of CH sweep steps (one global round trip
-  // per chunk, none inside a step: a load consumed inside the step loop would make every step
-  // wait for the ring stores before it, vmcnt counting both)
-  constexpr int CH = 64;  // = a.chunk
-  float* chunk = reinterpret_cast<float*>(row + 2 * RS);  // [2][CH][D]
-  auto st = [&](int k) { return fwd ? k : I - 1 - k; };  // input step of sweep step k
-  auto stage = [&](int c) {  // chunk c = sweep steps [c*CH, (c+1)*CH)
-    float* dstc = chunk + (c & 1) * CH * D;
-    for (int idx = tid; idx < CH * D; idx += kF4Threads) {
-      const int k = c * CH + idx / D;
-      dstc[idx] = k < I ? lg[(size_t)st(k) * D + idx % D] : 0.0f;
+  for (int i = 0; i < DC; ++i) dk[i] = dur[i];
+  auto st = [&](int k) { return FWD ? k : I - 1 - k; };  // input step of sweep step k
+  float pre[NPF];
+  // class log-probs through one descriptor: masked entries read past its end (zeros), so the
+  // loads need no exec mask and no default writes into registers with loads in flight
+  const __amdgpu_buffer_rsrc_t lg_r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(lg), (short)0, (int)((size_t)Imax * D * sizeof(float)), 0x00020000);
+  auto load_chunk = [&](int c) {  // chunk c = sweep steps [c CH, (c + 1) CH): class log-probs
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int idx = tid + kF4Threads * j;
+      const int k = c * CH + idx / DC, i = idx % DC;
+      const bool live = idx < CH * DC && i < D && k < I;
+      pre[j] = rbuf_ld1(lg_r, live ? (st(k) * D + i) * (int)sizeof(float) : (int)0x80000000, 0, 0);
     }
   };
-  auto weights = [&](int k) {  // class weights of sweep step k into wbuf[k & 1]
-    const float* srcc = chunk + ((k >> 6) & 1) * CH * D + (k & 63) * D;
-    for (int i = tid; i < D; i += kF4Threads) wbuf[(k & 1) * Dp + i] = xf_exp(srcc[i], cls_ok(i));
+  auto put_chunk = [&](int c) {  // ... converted into the chunk's LDS buffer
+    xf* dst = cw + (c & 1) * CH * DC;
+#pragma unroll
+    for (int j = 0; j < NPF; ++j) {
+      const int idx = tid + kF4Threads * j;
+      const int i = idx % DC;
+      if (idx < CH * DC) dst[idx] = i < D ? xf_exp(pre[j], a.allow_skip || i != a.zid) : xf_zero();
+    }
   };
-  stage(0);
-  stage(1);
-  lds_sync();
-  weights(0);
+  // both row buffers zero (the cells around every window stay zero: see the step)
+  for (int k = tid; k < 2 * RS; k += kF4Threads) row[k] = xf_zero();
+  load_chunk(0);
+  put_chunk(0);
+  load_chunk(1);
+  put_chunk(1);
   // first row: alpha[0] = 1 at total 0; beta[I] = 1 over window(I)
   int plo, phi;
-  f4_window(u, fwd ? 0 : I, plo, phi);
+  f4_window(u, FWD ? 0 : I, plo, phi);
   if (phi - plo + 1 > Wc) {
     if (tid == 0 && a.status) atomicOr(a.status, kStatusBadLength);
     return;
   }
-  if (tid < 2) rb(tid)[-1] = xf_zero();  // the always-zero cells left of each window
-  if (tid == 0) rb(0)[max(phi - plo + 1, 0)] = xf_zero();
+  lds_sync();  // (zeros before the first row's cells)
   for (int k = tid; k <= phi - plo; k += kF4Threads) {
-    rb(0)[k] = xf{0.5f, 1};
-    ws[(size_t)(fwd ? 0 : I) * Wc + k] = xf{0.5f, 1};
+    rw(0)[k] = xf{0.5f, 1};
+    ws[(size_t)(FWD ? 0 : I) * Wc + k] = xf{0.5f, 1};
   }
   lds_sync();
-  if (fwd && la) f4_log_row(la, rb(0), 0, 0, X);
-  for (int k = 1; k <= I; ++k) {
-    const int r = fwd ? k : I - k;  // row produced by this step
-    int lo, hi;
-    f4_window(u, r, lo, hi);
+  if (la) f4_log_row(la, rw(0), 0, 0, X);
+  // the utterance's workspace rows through one buffer descriptor (32-bit offsets: no 64-bit
+  // address arithmetic per cell)
+  const __amdgpu_buffer_rsrc_t ws_r = __builtin_amdgcn_make_buffer_rsrc(
+      ws, (short)0, (int)((size_t)(Imax + 1) * Wc * sizeof(xf)), 0x00020000);
+  int lo, hi;  // window of the row the next step produces (formed before the barrier)
+  f4_window(u, FWD ? 1 : I - 1, lo, hi);
+  // step k (1..I) produces row r = k (alpha) / I - k (beta) from the row of step k - 1 with the
+  // class weights of sweep step k - 1; false: a window beyond the row capacity (reported)
+  auto step = [&](int k) {
+    const int r = FWD ? k : I - k;
     if (hi - lo + 1 > Wc) {  // host sizing bug: report, poison the loss (uniform branch)
       if (tid == 0) {
         if (a.status) atomicOr(a.status, kStatusBadLength);
-        if (fwd) a.loss[b] = __builtin_nanf("");
+        if (FWD) a.loss[b] = __builtin_nanf("");
       }
-      return;
+      return false;
     }
-    if ((k & 63) == 0) stage((k >> 6) + 1);  // first read CH = 64 steps (barriers) from now
-    if (k < I) weights(k);                     // for the next iteration
-    const xf* w = wbuf + ((k - 1) & 1) * Dp;
-    const xf* src = rb((k - 1) & 1);
-    xf* dst = rb(k & 1);
+    const int ci = (k - 1) / CH, kk = (k - 1) - ci * CH;  // sweep step k - 1 in its chunk
+    const xf* w = cw + (ci & 1) * CH * DC + kk * DC;
+    const xf* srcw = rw((k - 1) & 1);
+    xf* dst = rw(k & 1);
     const bool pe = phi >= plo;  // previous window non-empty
     const int slo = pe ? plo : 0;
     const int span = pe ? phi - plo : -1;
-    xf* wrow = ws + (size_t)r * Wc;
+    // PADDED: cells whose every term lies outside the previous window are zero; the others have
+    // xr = x - slo within [0, span + dmax] (alpha) / [-dmax, span] (beta), so every term's cell
+    // lies within kF4Pad of the window
+    const int xlo = PADDED ? (FWD ? 0 : -dmax) : INT_MIN, xhi = PADDED ? (FWD ? span + dmax : span) : INT_MAX;
+    const int so = r * Wc * (int)sizeof(xf);
+    // this step's weights into registers before the cell loop (read once, ahead of the cells'
+    // row reads: measured 335 -> 323 us at configs[4] against reads inside the loop body)
+    xf wh[DC];
+#pragma unroll
+    for (int i = 0; i < DC; ++i) wh[i] = w[i];
     for (int x = lo + tid; x <= hi; x += kF4Threads) {
-      const xf v = fwd ? f4_cell<true, DC>(x, dr, w, src, slo, span)
-                       : f4_cell<false, DC>(x, dr, w, src, slo, span);
+      const int xr = x - slo;
+      const int xc = min(max(xr, xlo), xhi);
+      xf v = f4_cell<FWD, DC, PADDED>(xc, dk, wh, srcw, span);
+      if (PADDED && (xr != xc || !pe)) v = xf_zero();
       dst[x - lo] = v;
-      wrow[x - lo] = v;
+      rbuf_st2(f32x2{v.m, __builtin_bit_cast(float, v.e)}, ws_r, (x - lo) * (int)sizeof(xf), so, 0);
     }
-    if (tid == kF4Threads - 1) dst[max(hi - lo + 1, 0)] = xf_zero();  // (no cell writes there)
-    lds_sync();
-    if (fwd && la) f4_log_row(la + (size_t)r * X, dst, lo, hi, X);
+    // the cells right of the new window that the next step can reach: zero (a row two steps back
+    // may have left values there). Wave 7's lanes: idle unless the window exceeds 448 cells.
+    const int nz = PADDED ? dmax : 1;
+    const int zi = tid - (kF4Threads - 64);
+    if (zi >= 0 && zi < nz) dst[max(hi - lo + 1, 0) + zi] = xf_zero();
     plo = lo;
     phi = hi;
+    if (k < I) f4_window(u, FWD ? k + 1 : I - k - 1, lo, hi);  // (before the barrier)
+    lds_sync();
+    if (la) f4_log_row(la + (size_t)r * X, dst, plo, phi, X);
+    return true;
+  };
+  // chunk c = sweep steps [c CH, (c + 1) CH) = steps k in [c CH + 1, (c + 1) CH]. The weights of
+  // chunk c + 1 are loaded into registers as chunk c starts and put into LDS halfway through it
+  // (their buffer's last reader, chunk c - 1, is done by then): one wait for global memory per
+  // chunk, none inside a step (a load pending across steps would make every step wait for the
+  // previous step's row stores, vmcnt counting both)
+  for (int c = 0; c * CH < I; ++c) {
+    const bool next = c >= 1 && (c + 1) * CH < I;  // (chunks 0 and 1 are in place)
+    if (next) load_chunk(c + 1);
+    const int kmid = min(c * CH + CH / 2, I), kend = min((c + 1) * CH, I);
+    bool ok = true;
+    for (int k = c * CH + 1; ok && k <= kmid; ++k) ok = step(k);
+    if (!ok) return;
+    if (next) put_chunk(c + 1);  // (the next step's barrier publishes it before its first reader)
+    for (int k = kmid + 1; ok && k <= kend; ++k) ok = step(k);
+    if (!ok) return;
   }
-  if (!fwd) return;
+  if (!FWD) return;
   if (la)
     for (int r = I + 1; r <= Imax; ++r) f4_log_row(la + (size_t)r * X, nullptr, 0, -1, X);
   // Z over window(I): lane partials x mod 64, butterfly
   if (wave == 0) {
     xf acc = xf_zero();
-    const xf* rI = rb(I & 1);
+    const xf* rI = rw(I & 1);
     for (int x = plo + ((lane - plo) & 63); x <= phi; x += 64) acc = f4_add(acc, rI[x - plo]);
     acc = f4_butterfly(acc);
     if (lane == 0) {
       W.z[b] = acc;
       a.loss[b] = acc.m == 0.0f ? inf_loss : 0.0f - xf_log(acc);
     }
+  }
+}
+
+template <int DC>
+__global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const bool fwd = blockIdx.y == 0;
+  const int tid = threadIdx.x;
+  int* dur = reinterpret_cast<int*>(smem);
+  for (int i = tid; i < DC; i += kF4Threads) dur[i] = i < a.D ? a.table[i] : 0;
+  lds_sync();
+  F4Utt u;
+  if (!f4_setup(a, b, dur, u, fwd)) {
+    if (fwd) {
+      const float inf_loss = (a.flags & SSNT_FLAG_ZERO_INFINITY) ? 0.0f : __builtin_inff();
+      if (tid == 0) a.loss[b] = inf_loss;
+      if (a.log_alpha)
+        for (int r = 0; r <= a.Imax; ++r)
+          f4_log_row(a.log_alpha + b * (size_t)(a.Imax + 1) * a.X + (size_t)r * a.X, nullptr, 0, -1, a.X);
+    }
+    return;
+  }
+  const bool padded = u.dmax <= kF4Pad;  // (uniform)
+  if (fwd) {
+    if (padded) f4_sweep<DC, true, true>(a, smem, u, u.dmax);
+    else f4_sweep<DC, true, false>(a, smem, u, u.dmax);
+  } else {
+    if (padded) f4_sweep<DC, false, true>(a, smem, u, u.dmax);
+    else f4_sweep<DC, false, false>(a, smem, u, u.dmax);
   }
 }
 
@@ -472,11 +555,13 @@ int launch_v2_fwd_bwd(const V2FwdBwdArgs& in, hipStream_t st) {
   a.Wcap = (int)v2_fwd_bwd_wcap(a.X - 1, a.test_mode);
   const int Dp = a.D <= 8 ? 8 : a.D <= 16 ? 16 : a.D <= 32 ? 32 : 64;  // = DC
   const size_t head = (size_t)((Dp * 4 + 15) & ~15);
-  a.chunk = 64;  // sweep steps per staged chunk (a power of two)
-  const size_t lds = head + 2 * (size_t)Dp * sizeof(xf) + 2 * ((size_t)a.Wcap + 3) * sizeof(xf) +
-                     2 * (size_t)a.chunk * a.D * sizeof(float);
+  a.chunk = Dp <= 32 ? 64 : 32;  // = f4_chunk<DC>()
+  const size_t lds = head + 2 * (size_t)a.chunk * Dp * sizeof(xf) +
+                     2 * ((size_t)a.Wcap + 2 * kF4Pad + 2) * sizeof(xf);
   const size_t glds = head + (2 * (size_t)a.Wcap + 1) * sizeof(xf);
   if (lds > 160 * 1024 - 1024 || glds > 160 * 1024 - 1024) return SSNT_ERR_UNSUPPORTED;
+  // (a sweep addresses one utterance's workspace rows with 32-bit offsets)
+  if ((size_t)(a.Imax + 1) * a.Wcap * sizeof(xf) > 0x7fffffffu) return SSNT_ERR_UNSUPPORTED;
   if (!a.workspace || a.workspace_bytes < v2_fwd_bwd_workspace_bytes(a.B, a.Imax, a.X - 1, a.test_mode))
     return SSNT_ERR_WORKSPACE;
   if (a.D <= 8) return launch_f4<8>(a, lds, glds, st);

@@ -144,3 +144,36 @@ def test_band_mode_output_length_beyond_max_total(gpu, oracle, zero_infinity):
     _same(g, o, ["loss", "grad", "log_alpha", "log_beta"])
     assert np.all(g["loss"] == (0.0 if zero_infinity else np.inf))
     assert not g["grad"].any()
+
+
+F4_TABLES = [  # (name, duration_table): both cell forms and every class padding of the sweep
+    ("long_durations", [0, 3, 70, 5, 100, 2]),  # dmax 100 > 64: the clamped cell form
+    ("shuffled16", [7, 0, 12, 3, 9, 1, 15, 4, 2, 11, 6, 14, 8, 13, 10, 5]),
+    ("d20", list(range(0, 60, 3))),              # 32 class slots
+    ("d40", [(5 * i) % 64 for i in range(40)]),  # 64 class slots, 32-step weight chunks
+]
+
+
+@pytest.mark.parametrize("test_mode", [False, True])
+@pytest.mark.parametrize("name,table", F4_TABLES, ids=[t[0] for t in F4_TABLES])
+def test_duration_tables_bit_exact(gpu, oracle, name, table, test_mode):
+    # Non-identity duration tables, long ones beyond the sweep's padded row buffers, and I past
+    # two weight chunks (the staged chunks); utterance 4's band moves further per step than the
+    # longest duration (every cell of a row then reads outside the previous window: exact zeros)
+    table = np.array(table, np.int32)
+    D = len(table)
+    B, Imax = 5, 150
+    rng = np.random.default_rng(D)
+    logits = rng.standard_normal((B, Imax, D)).astype(np.float32) * np.float32(1.5)
+    m = logits.max(-1, keepdims=True)
+    logits = (logits - (m + np.log(np.exp(logits - m).sum(-1, keepdims=True)))).astype(np.float32)
+    I = np.array([150, 149, 97, 70, 20], np.int32)
+    O = np.array([int(table[rng.integers(0, D, size=i)].sum()) for i in I], np.int32)
+    O[4] = int(I[4]) * (int(table.max()) + 30)
+    mt = int(O[:4].max()) + (7 if test_mode else 0)
+    if test_mode:
+        O[4] = min(int(O[4]), mt)
+    g = _run(gpu, logits, table, I, O, 0, True, test_mode, mt)
+    o = oracle.v2_fwd_bwd(logits, table, I, O, mt, 0, True, test_mode, debug=True)
+    _same(g, o, ["loss", "grad", "log_alpha", "log_beta"])
+    assert np.isfinite(g["loss"][:4]).any()

@@ -16,7 +16,7 @@ while [ $# -ge 2 ]; do
 done
 wait
 for d in $L/var_*/; do
-  vo=$(ls $d/*.hip.o)
+  vo=$(ls $d/*.hip.o 2>/dev/null) || continue  # (make-built study libraries: var_desc*)
   objs=$(ls $L/obj/*.o | grep -v "/$(basename $vo .hip.o).o")
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libssnt_tts_c.so $vo $objs -Wl,-soname,libssnt_tts_c.so
 done
