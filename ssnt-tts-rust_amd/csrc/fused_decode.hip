@@ -96,11 +96,20 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 // store inside the step loop, whose wait-count merge would otherwise turn the row prefetch's
 // wait into a vmcnt(0) once per unrolled group -- and the backtrace reads them directly (no
 // separate history arrays).
+// waves per utterance of the register kernel: 64 candidates of a v2 / tone step rank on 4 waves
+// (each compares every candidate with 16 of the keys; the partial counts cross through LDS, one
+// barrier per step), everything else runs identically in each wave, and wave 0 alone writes
+// outputs. The 64 compares of one wave were a third of the step.
+constexpr int fused_waves(Variant v, int nmax, bool sel) {
+  return (nmax == 64 && v != Variant::V1 && !sel) ? 4 : 1;
+}
+
 struct RegLayout {
   size_t ring, hist, row, total;
   __host__ __device__ RegLayout(Variant v, int W, int T, int U, bool hist_lds, bool staged,
-                                bool whole) {
-    ring = 512;                                              // 64 sort keys (u64)
+                                bool whole, int waves) {
+    // per wave 64 sort keys (u64); with several waves the partial ranks, [2 steps][64][waves]
+    ring = 512 * (size_t)waves + (waves > 1 ? (size_t)2 * 64 * waves * 4 : 0);
     hist = ring + (size_t)kRec * (whole ? T : kChunk) * W * 4;
     const int nh = v == Variant::V2 ? 3 : 2;
     row = hist + ((hist_lds && !whole) ? (size_t)nh * T * W * 4 : 0);
@@ -119,17 +128,20 @@ struct RegLayout {
 // default occupancy target of 8 waves caps a wave at 64 VGPRs, which serialised the rank's
 // broadcast key reads into one LDS round trip per two keys).
 template <Variant V, bool STAGED, int NMAX, bool WHOLE, bool SEL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ __launch_bounds__(64 * fused_waves(V, NMAX, SEL)) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kV1 = V == Variant::V1, kV2 = V == Variant::V2;
+  constexpr int kNW = fused_waves(V, NMAX, SEL);
   const int b = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = kNW > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
   const int W = a.W, T = a.T, U = a.U;
   const int C = kV1 ? 2 : a.C;
   const int n = W * C;
-  const RegLayout L(V, W, T, U, hist_lds != 0, STAGED, WHOLE);
-  u64* keys = reinterpret_cast<u64*>(smem);
+  const RegLayout L(V, W, T, U, hist_lds != 0, STAGED, WHOLE, kNW);
+  u64* keys = reinterpret_cast<u64*>(smem) + 64 * wv;  // this wave's copy
+  int* xrank = reinterpret_cast<int*>(smem + 512 * kNW);  // [2][64][kNW] partial ranks
   int4* rec = reinterpret_cast<int4*>(smem + L.ring);  // 2 x int4 per (step, slot)
   int* h_br = reinterpret_cast<int*>(smem + L.hist);  // (T,W) parent slot (!WHOLE)
   int* h_aux = h_br + (size_t)T * W;                   // (T,W) v1: next_t; v2/tone: prediction
@@ -151,7 +163,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   const bool is_cand = c < n;
   const int w = is_cand ? c / C : 0;  // the beam this lane expands (generation order w*C + i)
   const int i = is_cand ? c - w * C : 0;
-  const bool writer = gbase == 0 && is_cand && i == 0;  // the lane that stages slot w's outputs
+  const bool writer = wv == 0 && gbase == 0 && is_cand && i == 0;  // stages slot w's outputs
   const int sid = a.special_id;
   // prediction code: class index, or C for the "not defined" padding candidate whose prediction
   // is the special id (equal to class sid when sid names a class: eq_ignore_parent compares it)
@@ -161,6 +173,26 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   const float o_over_i = (float)O / (float)I;
   const float upper_range = (float)O * 0.1f;
   const float lower_range = (float)O * 0.05f;
+
+  // v2 band of step s (src/v2.rs:94-111; uniform per step: every defined beam has t == s). The
+  // usize t + 1 converts to f32 like the int s + 1 for any s < 2^31 (the same integer, correctly
+  // rounded). Carried: step s forms step s + 1's band while its sort permutes are in flight.
+  struct Band {
+    int lb, ub;
+    bool overrun, last;
+  };
+  auto band_of = [&](int s) {
+    Band r;
+    const float diagonal = o_over_i * (float)(s + 1);
+    r.lb = f2i_sat(fmaxf(diagonal - lower_range, 0.0f));
+    r.ub = f2i_sat(fminf(diagonal + upper_range, (float)O));
+    const u64 t = (u64)s;
+    r.overrun = (I - (t + 1)) * 3 > O;
+    r.last = t == I - 1;
+    return r;
+  };
+  Band band{0, 0, false, false};
+  if constexpr (kV2) band = band_of(0);
 
   // state of beam w, replicated in its C candidate lanes
   float hist = 0.0f;
@@ -257,12 +289,8 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       // t = 0, an unfinished candidate of a defined beam moves to t + 1, and every other
       // candidate is finished (never defined again) -- so the band of src/v2.rs:94-111 is
       // uniform per step
-      const u64 t = (u64)s;
-      const float diagonal = o_over_i * (float)(t + 1);
-      const int lb = f2i_sat(fmaxf(diagonal - lower_range, 0.0f));
-      const int ub = f2i_sat(fminf(diagonal + upper_range, (float)O));
-      const bool overrun = (I - (t + 1)) * 3 > O;
-      const bool last = t == I - 1;
+      const int lb = band.lb, ub = band.ub;
+      const bool overrun = band.overrun, last = band.last;
       // the else-if chain of decode_beam_at as one conjunction
       const bool ok = (a.test_mode || (tot >= lb && tot <= ub)) && (a.test_mode || !overrun) &&
                       (!last || a.test_mode || tot == (int)O) && (a.allow_skip || i != sid);
@@ -289,6 +317,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     int g_lp, g_ntu, g_pk, g_tot;
     DSTAMP(0);
     if constexpr (SEL) {
+      if constexpr (kV2) band = band_of(s + 1);
       // ---- selection (src/lib.rs:161-168, src/v2.rs:280-308): only the first W kept candidates
       // of the sorted, deduplicated list (and the v2 diagonal one) are ever used, so they are
       // extracted one by one instead of ranking all n. A round takes the largest key among the
@@ -435,6 +464,22 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       }
       const auto r32 = __builtin_amdgcn_permlane32_swap(rank, rank, false, false);
       rank = (int)(r32[0] + r32[1]);
+    } else if constexpr (kNW > 1) {
+      // wave wv counts the keys [16 wv, 16 wv + 16) of its own copy; the partial counts meet in
+      // LDS (double-buffered by step parity: a wave a step ahead writes the other buffer) across
+      // one barrier that orders LDS only (no wait for the row prefetch's global loads)
+      keys[lane] = kSign ? 0ull - key : key;
+      lds_order();
+      const int part = count_beats(keys + (64 / kNW) * wv, std::integral_constant<int, 64 / kNW>{});
+      int* xr = xrank + (s & 1) * 64 * kNW;
+      xr[lane * kNW + wv] = part;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      static_assert(kNW == 4, "one 16-byte read of the partial counts");
+      const int4 pr = *reinterpret_cast<const int4*>(xr + lane * kNW);
+      rank = (pr.x + pr.y) + (pr.z + pr.w);
+      lds_order();
     } else {
       keys[lane] = kSign ? 0ull - key : key;
       lds_order();
@@ -459,6 +504,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     const int s_tot = kV2 ? perm_i(dst, tot) : 0;
     const int s_v0 = (kV1 && STAGED) ? perm_i(dst, __float_as_int(nv0)) : 0;
     const int s_v1 = (kV1 && STAGED) ? perm_i(dst, __float_as_int(nv1)) : 0;
+    if constexpr (kV2) band = band_of(s + 1);  // (independent of the permutes in flight)
     // ---- consecutive dedup, keep the first of each run (src/lib.rs:162; v2 adds the total)
     // every cross-lane read happens with the whole wave active: a DPP read of a lane that is
     // off in the exec mask returns the old value, so no shift may sit behind a short circuit
@@ -532,7 +578,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       }
     }
     if constexpr (!WHOLE) {
-      if (cs == kChunk - 1 || s == T - 1) flush(s - cs, cs + 1);
+      if (wv == 0 && (cs == kChunk - 1 || s == T - 1)) flush(s - cs, cs + 1);
     }
     DSTAMP(4);
 #ifdef SSNT_DIAG
@@ -555,9 +601,10 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     }
   }
   if (!ok) {
-    if (lane == 0 && a.status) atomicOr(a.status, kStatusNoCandidate);
+    if (wv == 0 && lane == 0 && a.status) atomicOr(a.status, kStatusNoCandidate);
     return;
   }
+  if (wv != 0) return;  // (the other waves' copies of the state are identical)
   if constexpr (WHOLE) flush(0, T);
 #ifdef SSNT_DIAG
   if (b == 0 && lane == 0)
@@ -737,11 +784,11 @@ constexpr bool use_select() { return false; }
 
 template <typename K>
 int launch_with_lds(K kernel, size_t lds, int B, hipStream_t st, const FusedDecodeArgs& a,
-                    int extra) {
+                    int extra, int waves = 1) {
   if (lds > 64 * 1024)  // per launch: the attribute is per device, and cheap to set
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
-  hipLaunchKernelGGL(kernel, dim3(B), dim3(64), lds, st, a, extra);
+  hipLaunchKernelGGL(kernel, dim3(B), dim3(64 * waves), lds, st, a, extra);
   return last_error();
 }
 
@@ -754,13 +801,14 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
   int rc = SSNT_OK;
   if (n <= 64) {
     const bool staged = V != Variant::V1 || 2 * (size_t)a.U <= 64 * (size_t)kV1Regs;
-    const bool whole = RegLayout(V, a.W, a.T, a.U, true, staged, true).total <= kMaxLds;
-    const bool hist_lds = whole || RegLayout(V, a.W, a.T, a.U, true, staged, false).total <= kMaxLds;
-    const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged, whole).total;
+    const bool sel = use_select();
+    const int nmax = n <= 8 ? 8 : n <= 16 ? 16 : n <= 32 ? 32 : 64;
+    const int nw = staged ? fused_waves(V, nmax, sel) : 1;
+    const bool whole = RegLayout(V, a.W, a.T, a.U, true, staged, true, nw).total <= kMaxLds;
+    const bool hist_lds = whole || RegLayout(V, a.W, a.T, a.U, true, staged, false, nw).total <= kMaxLds;
+    const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged, whole, nw).total;
     if (lds > kMaxLds) return SSNT_ERR_UNSUPPORTED;
     const int h = hist_lds ? 1 : 0;
-    const bool sel = use_select();
-    (void)sel;
     auto go = [&](auto kw, auto kc) {  // (NMAX, WHOLE) instance
       constexpr int NM = decltype(kw)::value;
       constexpr bool WH = decltype(kc)::value;
@@ -771,8 +819,10 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
         }
         return (int)SSNT_ERR_UNSUPPORTED;
       }
-      return SSNT_SEL_OR_RANK(sel, launch_with_lds(k_fused_reg<V, true, NM, WH, false>, lds, a.B, st, a, h),
-                              launch_with_lds(k_fused_reg<V, true, NM, WH, true>, lds, a.B, st, a, h));
+      return SSNT_SEL_OR_RANK(sel, launch_with_lds(k_fused_reg<V, true, NM, WH, false>, lds, a.B, st, a, h,
+                                                   fused_waves(V, NM, false)),
+                              launch_with_lds(k_fused_reg<V, true, NM, WH, true>, lds, a.B, st, a, h,
+                                              fused_waves(V, NM, true)));
     };
     auto pick = [&](auto kc) {
       if (n <= 8) return go(std::integral_constant<int, 8>{}, kc);
