@@ -848,6 +848,15 @@ int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t st, bool dense) {
   return dense ? launch_rows_k<2, true>(a, st) : launch_rows_k<2, false>(a, st);
 }
 
+#ifdef SSNT_DIAG
+// this file's copy of the per-wave cycle totals (stream_dev.h g_diag is per translation unit)
+int rows_diag_read(void* host, size_t bytes) {
+  if (bytes > sizeof(g_diag)) bytes = sizeof(g_diag);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? (int)bytes : -1;
+}
+#endif
+
 size_t rows_kernel_lds(int T, int U) {  // 0 when the kernel does not take the shape
   if (U > 128 || U <= 0) return 0;
   const int K = U <= 64 ? 1 : 2;

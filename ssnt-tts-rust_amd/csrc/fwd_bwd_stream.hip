@@ -35,6 +35,7 @@
 // Lanes past U (p0 = K*lane >= U) read a clamped valid position and write to a junk area; their
 // values never reach a valid position except multiplied by a masked (exact zero) factor.
 #include <hip/hip_runtime.h>
+#include <string.h>
 #include <limits.h>
 
 #include <atomic>
@@ -893,8 +894,15 @@ int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
 
 }  // namespace
 
+#if defined(SSNT_DIAG) && defined(SSNT_AB)
+int rows_diag_read(void* host, size_t bytes);  // fwd_bwd_rows.hip
+#endif
+
 int diag_read(void* host, size_t bytes) {
 #ifdef SSNT_DIAG
+#ifdef SSNT_AB
+  if (strncmp(last_fwd_bwd_dispatch(), "k_fwd_bwd_rows", 14) == 0) return rows_diag_read(host, bytes);
+#endif
   if (bytes > sizeof(g_diag)) bytes = sizeof(g_diag);
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
              ? (int)bytes : -1;
