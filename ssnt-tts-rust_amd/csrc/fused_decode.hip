@@ -108,8 +108,9 @@ struct RegLayout {
   size_t ring, hist, row, total;
   __host__ __device__ RegLayout(Variant v, int W, int T, int U, bool hist_lds, bool staged,
                                 bool whole, int waves) {
-    // per wave 64 sort keys (u64); with several waves the partial ranks, [2 steps][64][waves]
-    ring = 512 * (size_t)waves + (waves > 1 ? (size_t)2 * 64 * waves * 4 : 0);
+    // per wave 64 sort keys (u64); with several waves the partial ranks, [2 steps][64][waves];
+    // per wave 64 compacted kept records (int4)
+    ring = 512 * (size_t)waves + (waves > 1 ? (size_t)2 * 64 * waves * 4 : 0) + (size_t)1024 * waves;
     hist = ring + (size_t)kRec * (whole ? T : kChunk) * W * 4;
     const int nh = v == Variant::V2 ? 3 : 2;
     row = hist + ((hist_lds && !whole) ? (size_t)nh * T * W * 4 : 0);
@@ -142,6 +143,8 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   const RegLayout L(V, W, T, U, hist_lds != 0, STAGED, WHOLE, kNW);
   u64* keys = reinterpret_cast<u64*>(smem) + 64 * wv;  // this wave's copy
   int* xrank = reinterpret_cast<int*>(smem + 512 * kNW);  // [2][64][kNW] partial ranks
+  // this wave's compacted kept records (lp, ntu, pk, total) of the current step
+  int4* crec = reinterpret_cast<int4*>(smem + 512 * kNW + (kNW > 1 ? 2 * 64 * kNW * 4 : 0)) + 64 * wv;
   int4* rec = reinterpret_cast<int4*>(smem + L.ring);  // 2 x int4 per (step, slot)
   int* h_br = reinterpret_cast<int*>(smem + L.hist);  // (T,W) parent slot (!WHOLE)
   int* h_aux = h_br + (size_t)T * W;                   // (T,W) v1: next_t; v2/tone: prediction
@@ -498,18 +501,35 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     const int sp = c;  // sorted position of this lane within its replica
     const int pk = code | (fin << 7) | (w << 8);
     const int ntu = (nt << 16) | (nu & 0xffff);
-    const int s_lp = perm_i(dst, __float_as_int(lp));
-    const int s_ntu = perm_i(dst, ntu);
-    const int s_pk = perm_i(dst, pk);
-    const int s_tot = kV2 ? perm_i(dst, tot) : 0;
-    const int s_v0 = (kV1 && STAGED) ? perm_i(dst, __float_as_int(nv0)) : 0;
-    const int s_v1 = (kV1 && STAGED) ? perm_i(dst, __float_as_int(nv1)) : 0;
-    if constexpr (kV2) band = band_of(s + 1);  // (independent of the permutes in flight)
-    // ---- consecutive dedup, keep the first of each run (src/lib.rs:162; v2 adds the total)
-    // every cross-lane read happens with the whole wave active: a DPP read of a lane that is
-    // off in the exec mask returns the old value, so no shift may sit behind a short circuit
-    const int p_lp = wave_shr1(s_lp), p_ntu = wave_shr1(s_ntu), p_pk = wave_shr1(s_pk);
-    const int p_tot = kV2 ? wave_shr1(s_tot) : 0;
+    int s_lp, s_ntu, s_pk, s_tot, s_v0 = 0, s_v1 = 0, p_lp, p_ntu, p_pk, p_tot;
+    if constexpr (NMAX > 16 && !kV1) {
+      // sort through LDS records: each candidate stores its (lp, ntu, pk, total) at record
+      // `rank`, and sorted lane l reads records l and l - 1 (its predecessor, for the dedup) --
+      // one LDS round trip, in place of four permutes and four DPP shifts
+      crec[dst] = make_int4(__float_as_int(lp), ntu, pk, tot);
+      lds_order();
+      const int4 cr = crec[lane];
+      const int4 pr = crec[lane > 0 ? lane - 1 : 0];
+      lds_order();
+      s_lp = cr.x; s_ntu = cr.y; s_pk = cr.z; s_tot = kV2 ? cr.w : 0;
+      p_lp = pr.x; p_ntu = pr.y; p_pk = pr.z; p_tot = kV2 ? pr.w : 0;
+      if constexpr (kV2) band = band_of(s + 1);  // (independent of the reads in flight)
+    } else {
+      s_lp = perm_i(dst, __float_as_int(lp));
+      s_ntu = perm_i(dst, ntu);
+      s_pk = perm_i(dst, pk);
+      s_tot = kV2 ? perm_i(dst, tot) : 0;
+      if constexpr (kV1 && STAGED) {
+        s_v0 = perm_i(dst, __float_as_int(nv0));
+        s_v1 = perm_i(dst, __float_as_int(nv1));
+      }
+      if constexpr (kV2) band = band_of(s + 1);  // (independent of the permutes in flight)
+      // ---- consecutive dedup, keep the first of each run (src/lib.rs:162; v2 adds the total)
+      // every cross-lane read happens with the whole wave active: a DPP read of a lane that is
+      // off in the exec mask returns the old value, so no shift may sit behind a short circuit
+      p_lp = wave_shr1(s_lp); p_ntu = wave_shr1(s_ntu); p_pk = wave_shr1(s_pk);
+      p_tot = kV2 ? wave_shr1(s_tot) : 0;
+    }
     const bool same = (((s_pk ^ p_pk) & 0xff) == 0) & (__int_as_float(s_lp) == __int_as_float(p_lp)) &
                       (s_ntu == p_ntu) & (s_tot == p_tot);
     // bitwise, not short-circuit: the && form compiles to an exec-mask branch around the compare
@@ -540,6 +560,17 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       k = (dk >= 0 && w == W - 1) ? dk : (w < nkept ? w : w % nkept);
     }
     DSTAMP(2);
+    if constexpr (NMAX > 16 && !kV1) {
+      // compaction and slot fetch in one LDS round trip: kept element ck (its sorted lane's
+      // fields) is stored at record ck, and each lane reads record k (in-order DS within the
+      // wave: no barrier, and the sort's reads of these records are done; replica 0 writes,
+      // every replica reads the same records)
+      if (keep && gbase == 0) crec[__popcll(kmask & below)] = make_int4(s_lp, s_ntu, s_pk, s_tot);
+      lds_order();
+      const int4 kr = crec[k];
+      lds_order();
+      g_lp = kr.x; g_ntu = kr.y; g_pk = kr.z; g_tot = kV2 ? kr.w : 0;
+    } else {
     int srcl;  // sorted lane of kept element k
     if constexpr (NMAX <= 16) {
       srcl = gbase | kth_set_bit<NMAX>(kmask, k);
@@ -552,6 +583,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     if constexpr (kV1 && STAGED) {
       cv0 = __int_as_float(bperm_i(srcl, s_v0));
       cv1 = __int_as_float(bperm_i(srcl, s_v1));
+    }
     }
     }
     hist = __int_as_float(g_lp);
