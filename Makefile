@@ -22,7 +22,7 @@ AB_SRCS   := $(HIP_SRCS) $(CSRC)/fwd_bwd_pair.hip $(CSRC)/fwd_bwd_rows.hip
 HIP_HDRS  := $(wildcard $(CSRC)/*.h) include/ssnt_tts_c.h
 HIP_OBJS  := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(HIP_SRCS))
 
-all: lib lib-ab oracle
+all: lib lib-ab lib-diag lib-diag-fault oracle
 
 lib: $(LIB)
 oracle: $(ORACLE)
@@ -55,6 +55,17 @@ $(DIAGDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 	$(HIPCC) $(HIPFLAGS) -DSSNT_AB -DSSNT_DIAG -c $< -o $@
 $(DIAGDIR)/libssnt_tts_c.so: $(DIAG_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(DIAG_OBJS) -Wl,-soname,libssnt_tts_c.so
+
+# negative control of the diagnostic ring tags: converters label every slot with a wrong row
+# (tests/test_gpu_fwd_bwd.py::test_ring_tags_diag_build expects kStatusRingTag from it)
+DFDIR     := $(LIBDIR)/diagfault
+DF_OBJS   := $(patsubst $(CSRC)/%.hip,$(DFDIR)/obj/%.o,$(AB_SRCS))
+lib-diag-fault: $(DFDIR)/libssnt_tts_c.so
+$(DFDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DSSNT_AB -DSSNT_DIAG -DSSNT_DIAG_TAG_FAULT=1 -c $< -o $@
+$(DFDIR)/libssnt_tts_c.so: $(DF_OBJS)
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(DF_OBJS) -Wl,-soname,libssnt_tts_c.so
 
 # experiment build: one kernel instance (K=2, no log_obs), diag stamps, SSNT_EXP env knobs
 EXPDIR    := $(LIBDIR)/exp
@@ -100,4 +111,4 @@ $(ORACLE): oracle/ssnt_oracle.c
 clean:
 	rm -rf $(LIBDIR) oracle/build
 
-.PHONY: all lib lib-ab lib-diag lib-exp lib-expnd lib-var-desc oracle clean
+.PHONY: all lib lib-ab lib-diag lib-diag-fault lib-exp lib-expnd lib-var-desc oracle clean

@@ -25,7 +25,7 @@ int status_bits_to_code(int bits) {
   if (bits & kStatusDurationMismatch) return SSNT_ERR_DURATION_MISMATCH;
   if (bits & kStatusBadLength) return SSNT_ERR_BAD_LENGTH;
   if (bits & kStatusBadIndex) return SSNT_ERR_BAD_INDEX;
-  if (bits & kStatusTimeout) return SSNT_ERR_INTERNAL;
+  if (bits & (kStatusTimeout | kStatusRingTag)) return SSNT_ERR_INTERNAL;  // (tags: diag builds)
   return SSNT_OK;
 }
 

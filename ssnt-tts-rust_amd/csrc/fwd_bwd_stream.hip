@@ -133,6 +133,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   constexpr int R = (kRingSel % 100) ? (kRingSel % 100) : in_slots<OBS>();
   constexpr int kR2 = out_slots<OBS>() < R ? out_slots<OBS>() : R;
   static_assert(R % kR2 == 0, "ring sizes");
+#ifdef SSNT_DIAG
+  static_assert(R <= 32 && kR2 <= 16, "ring tags (Ctl)");
+#endif
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -357,6 +360,15 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         in.Bn = (s + 1 == M) ? lds_xrow<K>(cutb + pr) : lds_xrow<K>(outr + (size_t)(kR2 + (r - 1) % kR2) * Up + pr);
         if (OBS || lb) in.Bs = lds_xrow<K>(outr + (size_t)(kR2 + r % kR2) * Up + pr);
       }
+#ifdef SSNT_DIAG
+      tag_check(&ctl->ctag[d][r % R], r, a.status);
+      if (d == 0) {
+        if (s != M) tag_check(&ctl->rtag[0][s % kR2], s, a.status);
+      } else {
+        if (s + 1 != M) tag_check(&ctl->rtag[1][(r - 1) % kR2], r - 1, a.status);
+        if ((OBS || lb) && s != M) tag_check(&ctl->rtag[1][r % kR2], r, a.status);
+      }
+#endif
       cbar();
       ctr_st(&ctl->help[d][h], i + 1);  // ring rows read (in-order DS): reusable
     };
@@ -566,6 +578,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
             xrow_pack<K>(O, o);
             st_vec<2 * K>(reinterpret_cast<float*>(act ? sl + 16 * Up + 8 * p0 : junk_lane), o);
           }
+#ifdef SSNT_DIAG
+          tag_put(&ctl->ctag[d][r % R], r + kTagFault);
+#endif
           cbar();
           ctr_st(&ctl->conv[d][c], k + 1);
 #ifdef SSNT_DIAG
@@ -610,7 +625,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 #pragma unroll
   for (int j = 0; j < kR2; ++j)
     optr[j] = act ? outr + (size_t)(d * kR2 + j) * Up + p0 : reinterpret_cast<xf*>(junk_lane);
-  auto rd = [&](int j, XRow<K>& E, XRow<K>& Xx, XRow<K>& O) {
+  // slot j's factors (row: the stream row it should hold; check: a row the chain uses)
+  auto rd = [&](int j, XRow<K>& E, XRow<K>& Xx, XRow<K>& O, int row = 0, bool check = false) {
+    (void)row;
+    (void)check;
     if (EXP(10)) {  // experiment (timing only, wrong results): the chain reads no factors
 #pragma unroll
       for (int q = 0; q < K; ++q) {
@@ -637,6 +655,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         O.e[q] = 0;
       }
     }
+#ifdef SSNT_DIAG
+    if (check) tag_check(&ctl->ctag[d][j], row, a.status);
+#endif
   };
   constexpr int PF = EXPC(15) ? 4 : kChainPrefetch<OBS>(R);  // rows of factors in flight per chain
   static_assert(R % PF == 0 && PF < R, "prefetch buffers tile the ring");
@@ -682,7 +703,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     const int last = max(n - 1, 0);  // last stream row the chain reads
     wait_row(min(PF - 1, last));
     cbar();
-    sfor<PF>([&](auto J) { rd(decltype(J)::value, Eb[decltype(J)::value], Xb[decltype(J)::value], Ob[decltype(J)::value]); });
+    sfor<PF>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      rd(j, Eb[j], Xb[j], Ob[j], j, j <= last && n > 0);
+    });
     int help_seen = M + 1;  // first alpha ring row not yet released by the gradient waves
     // storage write pointer for alpha[r+1] (LDS mode)
     xf* wp = act ? rows + (size_t)Up + p0 : reinterpret_cast<xf*>(junk_lane);
@@ -718,8 +742,11 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         }
       } else {
         lds_xrow_st<K>(optr[(i + 1) % kR2], X);
+#ifdef SSNT_DIAG
+        tag_put(&ctl->rtag[0][(i + 1) % kR2], r + 1);
+#endif
       }
-      rd((i + PF) % R, Eb[par], Xb[par], Ob[par]);  // row r+PF (a stale slot past the end is dropped)
+      rd((i + PF) % R, Eb[par], Xb[par], Ob[par], r + PF, r + PF <= last);  // row r+PF (a stale slot past the end is dropped)
       if (EXP(14)) cbar();  // experiment 14: the reads issue here, not sunk toward their use
     };
     if (M == 0) ctr_rel(&ctl->a_ready, 1);
@@ -740,7 +767,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     const int last = S - 1;
     wait_row(min(PF, last));
     cbar();
-    sfor<PF>([&](auto J) { rd(decltype(J)::value, Eb[decltype(J)::value], Xb[decltype(J)::value], Ob[decltype(J)::value]); });
+    sfor<PF>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      rd(j, Eb[j], Xb[j], Ob[j], j, j <= last);
+    });
     int help_seen = S - M;  // first beta gradient row (stream rows) not finished
     xf* wp = act ? rows + (size_t)(S - 1) * Up + p0 : reinterpret_cast<xf*>(junk_lane);  // beta[S-1-r]
     const int wstep = act ? Up : 0;
@@ -760,6 +790,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         dg.mark_cut();
       } else {
         lds_xrow_st<K>(optr[i % kR2], X);
+#ifdef SSNT_DIAG
+        tag_put(&ctl->rtag[1][i % kR2], r);
+#endif
       }
       wp -= wstep;
     };
@@ -784,7 +817,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     if (c == 0) put(0, 0, std::integral_constant<int, 1>{});
     else put(0, 0, std::integral_constant<int, 0>{});
     cbar();
-    rd(PF % R, Eb[0], Xb[0], Ob[0]);
+    rd(PF % R, Eb[0], Xb[0], Ob[0], PF, PF <= last);
     auto step = [&](auto Ic, int base, bool live, auto Kd) {
       constexpr int i = decltype(Ic)::value;
       constexpr int par = i % PF;
@@ -796,7 +829,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
         beta_chain<K, OBS, (i % kChainNorm) == kChainNorm - 1>(X, Eb[par], Xb[par], Ob[par]);
       }
       put(r, i, Kd);
-      rd((i + PF) % R, Eb[par], Xb[par], Ob[par]);
+      rd((i + PF) % R, Eb[par], Xb[par], Ob[par], r + PF, r + PF <= last);
       if (EXP(14)) cbar();
     };
     cbar();

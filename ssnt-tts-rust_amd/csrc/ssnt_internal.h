@@ -15,6 +15,7 @@ constexpr int kStatusDurationMismatch = 1 << 1;  // upsample: sum(d) != output_l
 constexpr int kStatusBadLength = 1 << 2;         // fwd-bwd: step/pos length outside the tensor
 constexpr int kStatusBadIndex = 1 << 3;          // backtrace: branch index outside [0, W)
 constexpr int kStatusTimeout = 1 << 4;           // fwd-bwd: an intra-workgroup wait hit its bound
+constexpr int kStatusRingTag = 1 << 5;           // diagnostic builds only: a ring slot / row held another row
 
 int status_bits_to_code(int bits);
 

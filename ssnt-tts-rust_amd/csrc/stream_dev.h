@@ -16,7 +16,11 @@ namespace ssnt {
 namespace {
 constexpr int kMaxW = 4;  // max converter / gradient waves per direction
 constexpr int kSpinLimit = 1 << 22;
+#ifdef SSNT_DIAG
+constexpr size_t kCtlBytes = 512;  // + the ring tags below
+#else
 constexpr size_t kCtlBytes = 256;
+#endif
 
 struct Ctl {
   int conv[2][kMaxW];  // per direction / converter: rows of its share written to the ring
@@ -28,8 +32,30 @@ struct Ctl {
   int z_ready;       // Z published
   int pad;
   xf z;
+#ifdef SSNT_DIAG
+  // Diagnostic builds: the stream row each converter-ring slot holds (written after the slot's
+  // data, before the publishing counter) and the lattice / stream row each chain-ring row holds;
+  // every consumer reads the tag after its data and ORs kStatusRingTag into the status word when
+  // it is not the row it expected (tests/test_gpu_fwd_bwd.py::test_ring_tags_diag_build)
+  int ctag[2][32];
+  int rtag[2][16];
+#endif
 };
 static_assert(sizeof(Ctl) <= kCtlBytes, "control block");
+
+#ifdef SSNT_DIAG
+__device__ __forceinline__ void tag_put(int* t, int v) {
+  if ((threadIdx.x & 63) == 0) *t = v;
+}
+__device__ __forceinline__ void tag_check(const int* t, int want, int* status) {
+  if ((threadIdx.x & 63) == 0 && *t != want && status) atomicOr(status, kStatusRingTag);
+}
+// negative control (`make lib-diag-fault` only): converters label every slot with a wrong row
+#ifndef SSNT_DIAG_TAG_FAULT
+#define SSNT_DIAG_TAG_FAULT 0
+#endif
+constexpr int kTagFault = SSNT_DIAG_TAG_FAULT;
+#endif
 
 __device__ __forceinline__ int ctr_ld(const int* p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));

@@ -136,6 +136,38 @@ def test_reference_host_symbols_v2_tone(gpu, oracle, seed, host_sync):
     _eq(g, o, V1_KEYS, f"tone seed={seed}")
 
 
+def test_host_symbols_zero_copy_stress(gpu, oracle):
+    # the product's per-step symbols hand outputs back through coherent zero-copy
+    # staging and return when a flag kernel's completion word is seen. Check every output right
+    # after each return, over many back-to-back calls of varying shapes (the staging buffer is
+    # reused with every size) -- a stale line would show as a wrong beam here.
+    from ssnt_tts_amd import capi
+    n = 0
+    for seed in range(300):
+        if seed % 2 == 0:
+            c = dc.v1_case(seed, B=1)
+            W = c["h"].shape[1]
+            o = oracle.v1_step(c["h"], c["hist"], c["fin"], c["t"], c["u"], c["input_length"])
+            g = capi.ssnt_tts_beam_search_decode(c["h"][0], c["hist"][0], c["fin"][0], c["t"][0],
+                                                 c["u"][0], int(c["input_length"][0]), W)
+            _eq(g, {k: v[0] for k, v in o.items()}, V1_KEYS, f"v1 seed={seed}")
+        else:
+            c = dc.v2_case(seed)
+            B, W, D = c["h"].shape
+            o, rc = oracle.v2_step(c["h"], c["hist"], c["fin"], c["total"], c["table"], c["t"],
+                                   c["u"], c["input_length"], c["output_length"],
+                                   c["zero_duration_id"], c["allow_skip"], c["test_mode"])
+            if rc != 0:
+                continue
+            g = capi.ssnt_tts_v2_beam_search_decode(
+                c["h"], c["hist"], c["fin"], c["total"], c["table"], c["t"], c["u"],
+                c["input_length"], c["output_length"], B, W, D, c["zero_duration_id"],
+                c["allow_skip"], c["test_mode"])
+            _eq(g, o, V2_KEYS, f"v2 seed={seed}")
+        n += 1
+    assert n > 200
+
+
 def test_v1_two_step_appendix_b(gpu, golden):
     from ssnt_tts_amd import capi
     fx = golden["v1_two_step"]
