@@ -28,6 +28,14 @@ __device__ __forceinline__ int f2i_sat(float x) {
   return (int)x;
 }
 
+// the same as selects only (no exec-mask branch): below 2^31 the clamp is exact (the largest f32
+// under 2^31 is 2^31 - 128), at or above it the saturated value is selected, NaN gives 0
+__device__ __forceinline__ int f2i_sat_sel(float x) {
+  const int r = (int)fminf(fmaxf(x, -2147483648.0f), 2147483520.0f);
+  const int s = x >= 2147483648.0f ? 2147483647 : r;
+  return x != x ? 0 : s;
+}
+
 // Sort key of a log-prob: the IEEE order of the reference's comparison (src/lib.rs:161), so -0
 // and +0 share a key, extended to a total order by placing NaN below -inf. NaN inputs are
 // outside the parity contract; the total order only guarantees that ranks are

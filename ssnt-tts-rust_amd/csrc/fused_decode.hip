@@ -60,7 +60,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* base, unsign
 }
 constexpr int kV1Regs = 4;   // v1 lattice row floats per lane: the row is staged while 2U <= 256
 constexpr int kChunk = 32;   // per-step outputs staged in LDS and flushed every kChunk steps
-constexpr int kRec = 8;      // ints per staged output record (one per step and slot)
+constexpr int kRec = 4;      // ints per staged output record (one per step and slot)
 
 // lane of the k-th set bit (k from 0) of a mask whose bits all lie below NMAX: a binary search
 // on popcounts -- replaces the compaction permute and one bpermute (two LDS round trips)
@@ -90,8 +90,9 @@ __device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
 // LDS layout of k_fused_reg (bytes), shared with the host launcher.
-// Staged outputs are records of kRec ints per (step, slot): {prediction, log_prob, next_t,
-// next_u | next_fin, parent slot, next_total, -}, two 16-byte stores per step.
+// Staged outputs are records of kRec ints per (step, slot): the slot's packed state as the step
+// gathered it, {log_prob, next_t << 16 | next_u, code | fin << 7 | parent << 8, next_total} --
+// one 16-byte store per step with no repacking; the flush and the backtrace decode it.
 // WHOLE: the records of all T steps fit, so they are flushed once after the loop -- no global
 // store inside the step loop, whose wait-count merge would otherwise turn the row prefetch's
 // wait into a vmcnt(0) once per unrolled group -- and the backtrace reads them directly (no
@@ -180,22 +181,31 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   // v2 band of step s (src/v2.rs:94-111; uniform per step: every defined beam has t == s). The
   // usize t + 1 converts to f32 like the int s + 1 for any s < 2^31 (the same integer, correctly
   // rounded). Carried: step s forms step s + 1's band while its sort permutes are in flight.
+  // test_mode is folded in: the band then spans every int, nothing overruns and the last step
+  // needs no exact total (`exact`), so a candidate's check is one conjunction without branches.
   struct Band {
     int lb, ub;
-    bool overrun, last;
+    bool overrun, last, exact;
   };
+  const bool tmode = a.test_mode;
   auto band_of = [&](int s) {
     Band r;
     const float diagonal = o_over_i * (float)(s + 1);
-    r.lb = f2i_sat(fmaxf(diagonal - lower_range, 0.0f));
-    r.ub = f2i_sat(fminf(diagonal + upper_range, (float)O));
+    r.lb = f2i_sat_sel(fmaxf(diagonal - lower_range, 0.0f));
+    r.ub = f2i_sat_sel(fminf(diagonal + upper_range, (float)O));
+    r.lb = tmode ? (-2147483647 - 1) : r.lb;
+    r.ub = tmode ? 2147483647 : r.ub;
     const u64 t = (u64)s;
-    r.overrun = (I - (t + 1)) * 3 > O;
+    r.overrun = !tmode && (I - (t + 1)) * 3 > O;
     r.last = t == I - 1;
+    r.exact = !tmode && r.last;
     return r;
   };
-  Band band{0, 0, false, false};
+  Band band{0, 0, false, false, false};
   if constexpr (kV2) band = band_of(0);
+  const int o_int = (int)O;  // the final total is compared as `next_total == output_length as i32`
+  // the class rule of decode_beam_at (src/v2.rs:127-133), a per-lane constant
+  const bool class_ok = a.allow_skip || i != sid;
 
   // state of beam w, replicated in its C candidate lanes
   float hist = 0.0f;
@@ -232,19 +242,24 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     lds_order();
   }
 
+  // prediction of a packed code: class index, or the special id for the padding candidate
+  auto rec_pred = [&](int pk) {
+    const int pc = pk & 0x7f;
+    return pc == C ? sid : pc;
+  };
   auto flush = [&](int s0, int steps) {  // staged outputs of steps [s0, s0+steps), coalesced
     lds_order();
     const int cnt = steps * W;
     const size_t g0 = ((size_t)b * T + s0) * W;
     for (int k = lane; k < cnt; k += 64) {
-      const int4 r0 = rec[2 * k], r1 = rec[2 * k + 1];
-      a.prediction[g0 + k] = r0.x;
-      a.log_prob[g0 + k] = __int_as_float(r0.y);
-      a.next_t[g0 + k] = r0.z;
-      a.next_u[g0 + k] = r0.w & 0x7fffffff;
-      a.next_fin[g0 + k] = r0.w < 0;
-      a.beam_branch[g0 + k] = r1.x;
-      if constexpr (kV2) a.next_total[g0 + k] = r1.y;
+      const int4 r = rec[k];
+      a.prediction[g0 + k] = rec_pred(r.z);
+      a.log_prob[g0 + k] = __int_as_float(r.x);
+      a.next_t[g0 + k] = (int)((unsigned)r.y >> 16);
+      a.next_u[g0 + k] = r.y & 0xffff;
+      a.next_fin[g0 + k] = ((r.z >> 7) & 1) != 0;
+      a.beam_branch[g0 + k] = (r.z >> 8) & 63;
+      if constexpr (kV2) a.next_total[g0 + k] = r.w;
     }
     lds_order();
   };
@@ -266,7 +281,9 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // ---- candidate of this lane (decode_dev.h gen_candidate, one lane per candidate)
     // straight-line selects, no exec-mask branches (each branch costs exec save/restore and
     // splits the wait counts)
-    const bool defined = !bfin && as_usize(bt) < I;
+    // v2 / tone: every unfinished beam has t == s (each starts at t = 0 and an unfinished
+    // candidate moves to t + 1), so the test of t < I is the uniform s < I
+    const bool defined = kV1 ? (!bfin && as_usize(bt) < I) : (!bfin & ((u64)s < I));
     int valid, code, nt, nu, fin, tot = btot;
     float lp;
     if constexpr (kV1) {  // src/lib.rs:186-227
@@ -292,12 +309,11 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       // t = 0, an unfinished candidate of a defined beam moves to t + 1, and every other
       // candidate is finished (never defined again) -- so the band of src/v2.rs:94-111 is
       // uniform per step
-      const int lb = band.lb, ub = band.ub;
-      const bool overrun = band.overrun, last = band.last;
-      // the else-if chain of decode_beam_at as one conjunction
-      const bool ok = (a.test_mode || (tot >= lb && tot <= ub)) && (a.test_mode || !overrun) &&
-                      (!last || a.test_mode || tot == (int)O) && (a.allow_skip || i != sid);
-      const bool f = ok && last;
+      // the else-if chain of decode_beam_at as one conjunction (test_mode folded into the band),
+      // bitwise so that no term becomes an exec-mask branch
+      const bool ok = (tot >= band.lb) & (tot <= band.ub) & !band.overrun &
+                      (!band.exact | (tot == o_int)) & class_ok;
+      const bool f = ok & band.last;
       valid = ok; code = i; lp = hist + row[0];
       nt = f ? bt : bt + 1; nu = f ? bu : bu + 1; fin = f;
     }
@@ -310,6 +326,14 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     fin = defined ? fin : 1;
     tot = defined ? tot : btot;
     valid = valid && is_cand;
+    // v2: whether this candidate lies on the diagonal (src/v2.rs:283-289) -- a property of its own
+    // (total, next_t), so it is formed here and rides through the sort as bit 14 of the packed
+    // fields instead of being computed from the sorted fields on the step's critical path
+    int on_diag = 0;
+    if constexpr (kV2) {
+      const float diff = (float)tot - o_over_i * (float)(u64)(unsigned)nt;
+      on_diag = (!tmode & (valid != 0) & (diff >= -20.0f) & (diff <= 0.0f)) ? 1 : 0;
+    }
     // v1 staged: this candidate's row s+1 values at t = nt (read now, used by the next step)
     float nv0 = 0.0f, nv1 = 0.0f;
     if constexpr (kV1 && STAGED) {
@@ -408,6 +432,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     constexpr bool kSign = kJN >= 32;
     const u64 key = ((u64)(valid ? khi : 0u) << (kSign ? 31 : 32)) | (unsigned)(63 - c);
     int rank = 0;
+    int rank16 = -1;  // 16 * rank when the partial counts arrive premultiplied (four waves)
     // count the keys in kr[0, JN) (stored negated) that beat this lane's: key + (-key_j) has its
     // sign bit set iff key_j > key; the signs are shifted into a bit mask by v_alignbit and
     // counted per 32 -- no compare into an SGPR mask, so no VALU -> SGPR -> VALU hazard waits
@@ -475,13 +500,14 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       lds_order();
       const int part = count_beats(keys + (64 / kNW) * wv, std::integral_constant<int, 64 / kNW>{});
       int* xr = xrank + (s & 1) * 64 * kNW;
-      xr[lane * kNW + wv] = part;
+      xr[lane * kNW + wv] = part << 4;  // (premultiplied: the sum is the record's byte offset)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
       static_assert(kNW == 4, "one 16-byte read of the partial counts");
       const int4 pr = *reinterpret_cast<const int4*>(xr + lane * kNW);
-      rank = (pr.x + pr.y) + (pr.z + pr.w);
+      rank16 = (pr.x + pr.y) + (pr.z + pr.w);
+      rank = rank16 >> 4;
       lds_order();
     } else {
       keys[lane] = kSign ? 0ull - key : key;
@@ -499,14 +525,15 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // [0, nvalid) -- and the lanes past the bound keep their place (replicas: within the replica)
     const int dst = kRep ? (gbase | rank) : (lane < NMAX ? rank : lane);
     const int sp = c;  // sorted position of this lane within its replica
-    const int pk = code | (fin << 7) | (w << 8);
+    const int pk = code | (fin << 7) | (w << 8) | (on_diag << 14);
     const int ntu = (nt << 16) | (nu & 0xffff);
     int s_lp, s_ntu, s_pk, s_tot, s_v0 = 0, s_v1 = 0, p_lp, p_ntu, p_pk, p_tot;
     if constexpr (NMAX > 16 && !kV1) {
       // sort through LDS records: each candidate stores its (lp, ntu, pk, total) at record
       // `rank`, and sorted lane l reads records l and l - 1 (its predecessor, for the dedup) --
       // one LDS round trip, in place of four permutes and four DPP shifts
-      crec[dst] = make_int4(__float_as_int(lp), ntu, pk, tot);
+      int4* const crd = kNW > 1 ? reinterpret_cast<int4*>(reinterpret_cast<char*>(crec) + rank16) : crec + dst;
+      *crd = make_int4(__float_as_int(lp), ntu, pk, tot);
       lds_order();
       const int4 cr = crec[lane];
       const int4 pr = crec[lane > 0 ? lane - 1 : 0];
@@ -533,7 +560,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     const bool same = (((s_pk ^ p_pk) & 0xff) == 0) & (__int_as_float(s_lp) == __int_as_float(p_lp)) &
                       (s_ntu == p_ntu) & (s_tot == p_tot);
     // bitwise, not short-circuit: the && form compiles to an exec-mask branch around the compare
-    const bool keep = ((sp < nvalid ? 1 : 0) & ((sp == 0 ? 1 : 0) | (same ? 0 : 1))) != 0;
+    const bool keep = (sp < nvalid) & ((sp == 0) | !same);
     const u64 kmask = ballot(keep) & kGrp;
     const int nkept = __popcll(kmask);
     if constexpr (kV2) {  // assert_ne!(n_results, 0) (src/v2.rs:292); v1/tone always keep one
@@ -542,12 +569,9 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // ---- v2 diagonal injection (src/v2.rs:283-308): first kept candidate on the diagonal
     int dk = -1;
     if constexpr (kV2) {
-      if (!a.test_mode) {
-        const float diag = o_over_i * (float)(u64)((unsigned)s_ntu >> 16);
-        const float diff = (float)s_tot - diag;
-        const u64 dmask = ballot(keep && diff >= -20.0f && diff <= 0.0f) & kGrp;
-        if (dmask) dk = __popcll(kmask & ((1ull << (__ffsll((long long)dmask) - 1)) - 1ull));
-      }
+      // (the on-diagonal bit is 0 in test mode)
+      const u64 dmask = ballot(keep & (((s_pk >> 14) & 1) != 0)) & kGrp;
+      if (dmask) dk = __popcll(kmask & ((1ull << (__ffsll((long long)dmask) - 1)) - 1ull));
     }
     // ---- compaction (kept element k -> its sorted lane) and the cyclic pad
     int k;
@@ -557,7 +581,11 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       for (int r = 0; r < 3; ++r) kk = min(kk, kk - (unsigned)nkept);
       k = (int)kk;
     } else {
-      k = (dk >= 0 && w == W - 1) ? dk : (w < nkept ? w : w % nkept);
+      // nkept, W and dk are wave-uniform: both tests are scalar branches, and the modulo runs
+      // only when the kept list is shorter than the beam
+      k = w;
+      if (nkept < W) k = w % nkept;
+      if (dk >= 0) k = w == W - 1 ? dk : k;
     }
     DSTAMP(2);
     if constexpr (NMAX > 16 && !kV1) {
@@ -595,17 +623,11 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // ---- outputs of slot w (src/lib.rs:138-145), staged
     const int cs = WHOLE ? s : s % kChunk;
     if (writer) {
-      const int pc = g_pk & 0x7f;
-      const int pred = pc == C ? sid : pc;
-      const int parent = g_pk >> 8;
-      const int o = cs * W + w;
-      rec[2 * o] = make_int4(pred, __float_as_int(hist), bt, (int)(((unsigned)bu & 0x7fffffffu) | ((unsigned)bfin << 31)));
-      if constexpr (kV2) rec[2 * o + 1] = make_int4(parent, btot, 0, 0);
-      else reinterpret_cast<int*>(rec + 2 * o + 1)[0] = parent;  // (y..w never read)
+      rec[cs * W + w] = make_int4(g_lp, g_ntu, g_pk, kV2 ? g_tot : 0);
       if (!WHOLE && hist_lds) {
         const int hs = s * W + w;
-        h_br[hs] = parent;
-        h_aux[hs] = kV1 ? bt : pred;
+        h_br[hs] = (g_pk >> 8) & 63;
+        h_aux[hs] = kV1 ? bt : rec_pred(g_pk);
         if constexpr (kV2) h_tot[hs] = btot;
       }
     }
@@ -655,10 +677,10 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // history of (s, slot): parent, aux (v1: next_t; v2/tone: prediction), next_total
     auto hist_at = [&](int hs, int& parent, int& aux, int& tot) {
       if constexpr (WHOLE) {
-        const int4 r0 = rec[2 * hs], r1 = rec[2 * hs + 1];
-        parent = r1.x;
-        aux = kV1 ? r0.z : r0.x;
-        tot = r1.y;
+        const int4 r = rec[hs];
+        parent = (r.z >> 8) & 63;
+        aux = kV1 ? (int)((unsigned)r.y >> 16) : rec_pred(r.z);
+        tot = r.w;
       } else {
         parent = h_br[hs];
         aux = h_aux[hs];

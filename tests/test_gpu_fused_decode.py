@@ -240,13 +240,14 @@ def test_nan_inputs_stay_in_range(gpu, oracle, kind):
 
 
 # Long decodes: the register kernel's two other history layouts. WHOLE (every per-step record in
-# LDS, one flush after the loop) holds while T*W <= ~4700 (RegLayout in fused_decode.hip); past
-# that the records are flushed every 32 steps with the (parent, aux[, total]) history kept in
-# LDS for the in-launch backtrace; past ~150 KB of history (nh*4*T*W bytes) the history stays in
-# the global outputs and k_fused_paths backtraces from there.
+# LDS as 16-byte records, one flush after the loop) holds while 16*T*W fits beside the rank
+# buffers (T*W <= ~9300 for one wave, ~9000 for the four-wave v2 step; RegLayout in
+# fused_decode.hip); past that the records are flushed every 32 steps with the (parent, aux[,
+# total]) history kept in LDS for the in-launch backtrace; past ~150 KB of history (nh*4*T*W
+# bytes) the history stays in the global outputs and k_fused_paths backtraces from there.
 @pytest.mark.parametrize("T,U,W,ctx", [
-    (1500, 80, 4, "chunked flush, history in LDS, staged rows"),
-    (1300, 300, 4, "chunked flush, history in LDS, rows from HBM"),
+    (3000, 80, 4, "chunked flush, history in LDS, staged rows"),
+    (2600, 300, 4, "chunked flush, history in LDS, rows from HBM"),
     (700, 40, 32, "history beyond LDS: k_fused_paths"),
 ])
 @pytest.mark.parametrize("tie_rich", [False, True])
@@ -266,10 +267,10 @@ def test_v1_long_history_layouts(gpu, oracle, T, U, W, ctx, tie_rich):
 
 
 def test_v2_long_chunked_flush(gpu, oracle):
-    # I=1500 steps at W=4, D=16 (T*W = 6000): chunked flush with the 3-array history in LDS; the
-    # band and exact-length rules decide every step (O = 5 I)
-    lg, il, ol, _ = _config5(oracle, 31, B=4, I=1500, O=7500, D=16, W=4)
-    _v2(gpu, oracle, lg, np.arange(16, dtype=np.int32), il, ol, 0, False, False, "v2 I=1500")
+    # I=2800 steps at W=4, D=16 (T*W = 11200): chunked flush with the 3-array history in LDS;
+    # the band and exact-length rules decide every step (O = 5 I)
+    lg, il, ol, _ = _config5(oracle, 31, B=4, I=2800, O=14000, D=16, W=4)
+    _v2(gpu, oracle, lg, np.arange(16, dtype=np.int32), il, ol, 0, False, False, "v2 I=2800")
 
 
 def test_v2_history_beyond_lds(gpu, oracle):
@@ -283,7 +284,7 @@ def test_v2_history_beyond_lds(gpu, oracle):
 
 
 @pytest.mark.parametrize("T,W,C,ctx", [
-    (1500, 4, 5, "chunked flush, history in LDS"),
+    (3000, 4, 5, "chunked flush, history in LDS"),
     (500, 64, 1, "history beyond LDS: k_fused_paths"),
 ])
 def test_tone_long_history_layouts(gpu, oracle, T, W, C, ctx):
