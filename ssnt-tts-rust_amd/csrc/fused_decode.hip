@@ -180,7 +180,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
 
   // v2 band of step s (src/v2.rs:94-111; uniform per step: every defined beam has t == s). The
   // usize t + 1 converts to f32 like the int s + 1 for any s < 2^31 (the same integer, correctly
-  // rounded). Carried: step s forms step s + 1's band while its sort permutes are in flight.
+  // rounded).
   // test_mode is folded in: the band then spans every int, nothing overruns and the last step
   // needs no exact total (`exact`), so a candidate's check is one conjunction without branches.
   struct Band {
@@ -202,7 +202,27 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     return r;
   };
   Band band{0, 0, false, false, false};
-  if constexpr (kV2) band = band_of(0);
+  // the bands of 64 consecutive steps, one per lane (lane l: step 64 j + l), formed once per 64
+  // steps; step s reads its own with three v_readlane instead of ~22 instructions of f32 band
+  // arithmetic per step
+  int bl_lb = 0, bl_ub = 0, bl_fl = 0;
+  auto band_block = [&](int s0) {
+    const Band r = band_of(s0 + lane);
+    bl_lb = r.lb;
+    bl_ub = r.ub;
+    bl_fl = (r.overrun ? 1 : 0) | (r.last ? 2 : 0) | (r.exact ? 4 : 0);
+  };
+  auto band_at = [&](int s) {
+    const int l = s & 63;
+    Band r;
+    r.lb = readlane_i(bl_lb, l);
+    r.ub = readlane_i(bl_ub, l);
+    const int fl = readlane_i(bl_fl, l);
+    r.overrun = (fl & 1) != 0;
+    r.last = (fl & 2) != 0;
+    r.exact = (fl & 4) != 0;
+    return r;
+  };
   const int o_int = (int)O;  // the final total is compared as `next_total == output_length as i32`
   // the class rule of decode_beam_at (src/v2.rs:127-133), a per-lane constant
   const bool class_ok = a.allow_skip || i != sid;
@@ -278,6 +298,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       lds_order();
     }
     (void)row;
+    if constexpr (kV2) band = band_at(s);
     // ---- candidate of this lane (decode_dev.h gen_candidate, one lane per candidate)
     // straight-line selects, no exec-mask branches (each branch costs exec save/restore and
     // splits the wait counts)
@@ -344,7 +365,6 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     int g_lp, g_ntu, g_pk, g_tot;
     DSTAMP(0);
     if constexpr (SEL) {
-      if constexpr (kV2) band = band_of(s + 1);
       // ---- selection (src/lib.rs:161-168, src/v2.rs:280-308): only the first W kept candidates
       // of the sorted, deduplicated list (and the v2 diagonal one) are ever used, so they are
       // extracted one by one instead of ranking all n. A round takes the largest key among the
@@ -540,7 +560,6 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       lds_order();
       s_lp = cr.x; s_ntu = cr.y; s_pk = cr.z; s_tot = kV2 ? cr.w : 0;
       p_lp = pr.x; p_ntu = pr.y; p_pk = pr.z; p_tot = kV2 ? pr.w : 0;
-      if constexpr (kV2) band = band_of(s + 1);  // (independent of the reads in flight)
     } else {
       s_lp = perm_i(dst, __float_as_int(lp));
       s_ntu = perm_i(dst, ntu);
@@ -550,7 +569,6 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
         s_v0 = perm_i(dst, __float_as_int(nv0));
         s_v1 = perm_i(dst, __float_as_int(nv1));
       }
-      if constexpr (kV2) band = band_of(s + 1);  // (independent of the permutes in flight)
       // ---- consecutive dedup, keep the first of each run (src/lib.rs:162; v2 adds the total)
       // every cross-lane read happens with the whole wave active: a DPP read of a lane that is
       // off in the exec mask returns the old value, so no shift may sit behind a short circuit
@@ -643,6 +661,10 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
 
   bool ok = true;
   for (int s0 = 0; s0 < T && ok; s0 += kAhead) {  // unrolled by the ring: register indices fixed
+    if constexpr (kV2) {
+      static_assert(64 % kAhead == 0, "a band block starts at a loop iteration");
+      if ((s0 & 63) == 0) band_block(s0);
+    }
 #pragma unroll
     for (int k = 0; k < kAhead; ++k) {
       // the refill is unconditional (clamped rows past T): a load skipped on some path would

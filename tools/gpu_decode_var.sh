@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# GPU box: configs[4] v2 / tone fused-decode times of the product library and each named var_*
+# GPU box: configs[4] v2 / tone and configs[2] v1 fused-decode times of the product library and each named var_*
 # build, alternating (the bench_configs timers; CPU baseline skipped). Tuning study only.
 set -uo pipefail
 cd "$(dirname "$0")/.."
@@ -14,6 +14,7 @@ import bench_configs as bc
 bc.cpu_time = lambda fn, min_s=0: 1.0
 v2 = bc.v2_decode_config(64, 400, 2000, 16, 4, iters=10)
 tone = bc.tone_decode_config(64, 400, 5, 4, iters=10)
-print(sys.argv[1], "v2", round(v2["gpu_us"], 1), "tone", round(tone["gpu_us"], 1))
+v1 = bc.decode_config(256, 200, 80, 4, iters=10)
+print(sys.argv[1], "v2", round(v2["gpu_us"], 1), "tone", round(tone["gpu_us"], 1), "v1", round(v1["gpu_us"], 1))
 PY
 done
