@@ -85,6 +85,14 @@ __device__ __forceinline__ int kth_set_bit(u64 m64, int k) {
 // compare per call)
 __device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// per lane: bit `lane` of the wave-uniform mask m selects if_set, else if_clear (one v_cndmask with
+// m as its lane mask; the compiler would shift and compare per lane)
+__device__ __forceinline__ int mask_sel(u64 m, int if_set, int if_clear) {
+  int r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+  return r;
+}
+
 // One wave per workgroup: LDS operations of a wave complete in order, so a write followed by a
 // read of the same location needs no barrier -- only the compiler must keep the order.
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
@@ -110,8 +118,8 @@ struct RegLayout {
   __host__ __device__ RegLayout(Variant v, int W, int T, int U, bool hist_lds, bool staged,
                                 bool whole, int waves) {
     // per wave 64 sort keys (u64); with several waves the partial ranks, [2 steps][64][waves];
-    // per wave 64 compacted kept records (int4)
-    ring = 512 * (size_t)waves + (waves > 1 ? (size_t)2 * 64 * waves * 4 : 0) + (size_t)1024 * waves;
+    // per wave 64 compacted kept records (int4) and 64 spare ones (the stores of lanes not kept)
+    ring = 512 * (size_t)waves + (waves > 1 ? (size_t)2 * 64 * waves * 4 : 0) + (size_t)2048 * waves;
     hist = ring + (size_t)kRec * (whole ? T : kChunk) * W * 4;
     const int nh = v == Variant::V2 ? 3 : 2;
     row = hist + ((hist_lds && !whole) ? (size_t)nh * T * W * 4 : 0);
@@ -145,7 +153,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   u64* keys = reinterpret_cast<u64*>(smem) + 64 * wv;  // this wave's copy
   int* xrank = reinterpret_cast<int*>(smem + 512 * kNW);  // [2][64][kNW] partial ranks
   // this wave's compacted kept records (lp, ntu, pk, total) of the current step
-  int4* crec = reinterpret_cast<int4*>(smem + 512 * kNW + (kNW > 1 ? 2 * 64 * kNW * 4 : 0)) + 64 * wv;
+  int4* crec = reinterpret_cast<int4*>(smem + 512 * kNW + (kNW > 1 ? 2 * 64 * kNW * 4 : 0)) + 128 * wv;
   int4* rec = reinterpret_cast<int4*>(smem + L.ring);  // 2 x int4 per (step, slot)
   int* h_br = reinterpret_cast<int*>(smem + L.hist);  // (T,W) parent slot (!WHOLE)
   int* h_aux = h_br + (size_t)T * W;                   // (T,W) v1: next_t; v2/tone: prediction
@@ -579,7 +587,20 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
                       (s_ntu == p_ntu) & (s_tot == p_tot);
     // bitwise, not short-circuit: the && form compiles to an exec-mask branch around the compare
     const bool keep = (sp < nvalid) & ((sp == 0) | !same);
-    const u64 kmask = ballot(keep) & kGrp;
+    u64 kmask;
+    if constexpr (NMAX > 16 && !kV1) {
+      // the same mask from direct compare ballots: sorted positions [0, nvalid) (a scalar mask),
+      // kept at position 0 or where the fields differ from the predecessor's -- no per-lane bool
+      // materialised and ballotted again
+      // (one ballot per compare: a ballot of a combined bool is materialised and compared again)
+      const u64 differ = ballot(((s_pk ^ p_pk) & 0xff) != 0) |
+                         ballot(__int_as_float(s_lp) != __int_as_float(p_lp)) | ballot(s_ntu != p_ntu) |
+                         ballot(s_tot != p_tot);
+      const u64 lowv = nvalid >= 64 ? ~0ull : ((1ull << nvalid) - 1ull);
+      kmask = lowv & (differ | 1ull) & kGrp;
+    } else {
+      kmask = ballot(keep) & kGrp;
+    }
     const int nkept = __popcll(kmask);
     if constexpr (kV2) {  // assert_ne!(n_results, 0) (src/v2.rs:292); v1/tone always keep one
       if (nkept == 0) return false;
@@ -588,7 +609,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     int dk = -1;
     if constexpr (kV2) {
       // (the on-diagonal bit is 0 in test mode)
-      const u64 dmask = ballot(keep & (((s_pk >> 14) & 1) != 0)) & kGrp;
+      const u64 dmask = ballot((s_pk & (1 << 14)) != 0) & kmask;
       if (dmask) dk = __popcll(kmask & ((1ull << (__ffsll((long long)dmask) - 1)) - 1ull));
     }
     // ---- compaction (kept element k -> its sorted lane) and the cyclic pad
@@ -611,7 +632,11 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       // fields) is stored at record ck, and each lane reads record k (in-order DS within the
       // wave: no barrier, and the sort's reads of these records are done; replica 0 writes,
       // every replica reads the same records)
-      if (keep && gbase == 0) crec[__popcll(kmask & below)] = make_int4(s_lp, s_ntu, s_pk, s_tot);
+      // kept lane of replica 0 -> record mbcnt(kmask) (the kept lanes before it); every other lane
+      // (dropped, or a later replica's: kmask's bits lie below NMAX) stores to its own spare
+      // record 64 + lane, so the store needs no exec mask
+      const int cidx = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(kmask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)kmask, 0u));
+      crec[mask_sel(kmask, cidx, 64 + lane)] = make_int4(s_lp, s_ntu, s_pk, s_tot);
       lds_order();
       const int4 kr = crec[k];
       lds_order();
