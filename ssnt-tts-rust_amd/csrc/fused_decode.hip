@@ -118,8 +118,10 @@ struct RegLayout {
   __host__ __device__ RegLayout(Variant v, int W, int T, int U, bool hist_lds, bool staged,
                                 bool whole, int waves) {
     // per wave 64 sort keys (u64); with several waves the partial ranks, [2 steps][64][waves];
-    // per wave 64 compacted kept records (int4) and 64 spare ones (the stores of lanes not kept)
-    ring = 512 * (size_t)waves + (waves > 1 ? (size_t)2 * 64 * waves * 4 : 0) + (size_t)2048 * waves;
+    // per wave 64 compacted kept records (int4) and 64 spare ones (the stores of lanes not kept),
+    // then per wave the 128 v1 second row values
+    ring = 512 * (size_t)waves + (waves > 1 ? (size_t)2 * 64 * waves * 4 : 0) + (size_t)2048 * waves +
+           (size_t)512 * waves;
     hist = ring + (size_t)kRec * (whole ? T : kChunk) * W * 4;
     const int nh = v == Variant::V2 ? 3 : 2;
     row = hist + ((hist_lds && !whole) ? (size_t)nh * T * W * 4 : 0);
@@ -143,6 +145,9 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kV1 = V == Variant::V1, kV2 = V == Variant::V2;
   constexpr int kNW = fused_waves(V, NMAX, SEL);
+  // sort and compaction through LDS records (v2 / tone beyond 16 candidates, staged v1); the
+  // other forms permute the fields across lanes
+  constexpr bool kRecs = (NMAX > 16 && !kV1) || (kV1 && STAGED);
   const int b = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int wv = kNW > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
@@ -154,6 +159,8 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   int* xrank = reinterpret_cast<int*>(smem + 512 * kNW);  // [2][64][kNW] partial ranks
   // this wave's compacted kept records (lp, ntu, pk, total) of the current step
   int4* crec = reinterpret_cast<int4*>(smem + 512 * kNW + (kNW > 1 ? 2 * 64 * kNW * 4 : 0)) + 128 * wv;
+  // v1: the second staged row value of each record, 128 per wave after the waves' records
+  int* crec2 = reinterpret_cast<int*>(smem + 512 * kNW + (kNW > 1 ? 2 * 64 * kNW * 4 : 0) + 2048 * kNW) + 128 * wv;
   int4* rec = reinterpret_cast<int4*>(smem + L.ring);  // 2 x int4 per (step, slot)
   int* h_br = reinterpret_cast<int*>(smem + L.hist);  // (T,W) parent slot (!WHOLE)
   int* h_aux = h_br + (size_t)T * W;                   // (T,W) v1: next_t; v2/tone: prediction
@@ -556,18 +563,22 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     const int pk = code | (fin << 7) | (w << 8) | (on_diag << 14);
     const int ntu = (nt << 16) | (nu & 0xffff);
     int s_lp, s_ntu, s_pk, s_tot, s_v0 = 0, s_v1 = 0, p_lp, p_ntu, p_pk, p_tot;
-    if constexpr (NMAX > 16 && !kV1) {
+    if constexpr (kRecs) {
       // sort through LDS records: each candidate stores its (lp, ntu, pk, total) at record
       // `rank`, and sorted lane l reads records l and l - 1 (its predecessor, for the dedup) --
-      // one LDS round trip, in place of four permutes and four DPP shifts
+      // one LDS round trip, in place of four permutes and four DPP shifts. v1 carries its two
+      // staged row values instead of the total: the first in the record, the second beside it.
       int4* const crd = kNW > 1 ? reinterpret_cast<int4*>(reinterpret_cast<char*>(crec) + rank16) : crec + dst;
-      *crd = make_int4(__float_as_int(lp), ntu, pk, tot);
+      *crd = make_int4(__float_as_int(lp), ntu, pk, kV1 ? __float_as_int(nv0) : tot);
+      if constexpr (kV1) crec2[dst] = __float_as_int(nv1);
       lds_order();
       const int4 cr = crec[lane];
       const int4 pr = crec[lane > 0 ? lane - 1 : 0];
+      if constexpr (kV1) s_v1 = crec2[lane];
       lds_order();
       s_lp = cr.x; s_ntu = cr.y; s_pk = cr.z; s_tot = kV2 ? cr.w : 0;
       p_lp = pr.x; p_ntu = pr.y; p_pk = pr.z; p_tot = kV2 ? pr.w : 0;
+      if constexpr (kV1) s_v0 = cr.w;
     } else {
       s_lp = perm_i(dst, __float_as_int(lp));
       s_ntu = perm_i(dst, ntu);
@@ -588,7 +599,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // bitwise, not short-circuit: the && form compiles to an exec-mask branch around the compare
     const bool keep = (sp < nvalid) & ((sp == 0) | !same);
     u64 kmask;
-    if constexpr (NMAX > 16 && !kV1) {
+    if constexpr (kRecs || NMAX <= 16) {  // (the v1 permute form beyond 16 uses `keep` itself)
       // the same mask from direct compare ballots: sorted positions [0, nvalid) (a scalar mask),
       // kept at position 0 or where the fields differ from the predecessor's -- no per-lane bool
       // materialised and ballotted again
@@ -627,7 +638,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       if (dk >= 0) k = w == W - 1 ? dk : k;
     }
     DSTAMP(2);
-    if constexpr (NMAX > 16 && !kV1) {
+    if constexpr (kRecs) {
       // compaction and slot fetch in one LDS round trip: kept element ck (its sorted lane's
       // fields) is stored at record ck, and each lane reads record k (in-order DS within the
       // wave: no barrier, and the sort's reads of these records are done; replica 0 writes,
@@ -636,11 +647,15 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       // (dropped, or a later replica's: kmask's bits lie below NMAX) stores to its own spare
       // record 64 + lane, so the store needs no exec mask
       const int cidx = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(kmask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)kmask, 0u));
-      crec[mask_sel(kmask, cidx, 64 + lane)] = make_int4(s_lp, s_ntu, s_pk, s_tot);
+      const int widx = mask_sel(kmask, cidx, 64 + lane);
+      crec[widx] = make_int4(s_lp, s_ntu, s_pk, kV1 ? s_v0 : s_tot);
+      if constexpr (kV1) crec2[widx] = s_v1;
       lds_order();
       const int4 kr = crec[k];
+      if constexpr (kV1) cv1 = __int_as_float(crec2[k]);
       lds_order();
       g_lp = kr.x; g_ntu = kr.y; g_pk = kr.z; g_tot = kV2 ? kr.w : 0;
+      if constexpr (kV1) cv0 = __int_as_float(kr.w);
     } else {
     int srcl;  // sorted lane of kept element k
     if constexpr (NMAX <= 16) {
