@@ -35,6 +35,10 @@ namespace {
 using namespace dec;
 
 constexpr int kAhead = 8;    // input rows in flight
+// the rank counts by sign bits from this many compares per lane up (tuning knob: -D override)
+#ifndef SSNT_DEC_SIGN_MIN
+#define SSNT_DEC_SIGN_MIN 16
+#endif
 
 // Diagnostic build only (-DSSNT_DIAG, `make lib-diag`): s_memtime cycle totals of the register
 // kernel's step phases for utterance 0 (tools/diag_decode.py): 0 candidate generation, 1 rank /
@@ -464,7 +468,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // kSign (>= 32 compares per lane): a 63-bit key (high word shifted by 31), so a difference of
     // two keys never overflows and its sign bit is the comparison; else (khi, 63 - c) as a pair
     constexpr int kJN = kRep8 ? 1 : NMAX / kReps;
-    constexpr bool kSign = kJN >= 32;
+    constexpr bool kSign = kJN >= SSNT_DEC_SIGN_MIN;
     const u64 key = ((u64)(valid ? khi : 0u) << (kSign ? 31 : 32)) | (unsigned)(63 - c);
     int rank = 0;
     int rank16 = -1;  // 16 * rank when the partial counts arrive premultiplied (four waves)
@@ -681,7 +685,8 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // ---- outputs of slot w (src/lib.rs:138-145), staged
     const int cs = WHOLE ? s : s % kChunk;
     if (writer) {
-      rec[cs * W + w] = make_int4(g_lp, g_ntu, g_pk, kV2 ? g_tot : 0);
+      // (.w is read back for v2 only: v1 stores its carried row value there as gathered)
+      rec[cs * W + w] = make_int4(g_lp, g_ntu, g_pk, kV2 ? g_tot : (kV1 && kRecs) ? __float_as_int(cv0) : 0);
       if (!WHOLE && hist_lds) {
         const int hs = s * W + w;
         h_br[hs] = (g_pk >> 8) & 63;
