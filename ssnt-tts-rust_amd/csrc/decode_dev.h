@@ -41,8 +41,10 @@ __device__ __forceinline__ int f2i_sat_sel(float x) {
 // outside the parity contract; the total order only guarantees that ranks are
 // a permutation (every output stays in range). Never 0: 0 marks "no candidate".
 __device__ __forceinline__ unsigned lp_key(float x) {  // selects only: no exec-mask branch
-  const unsigned bits = x == 0.0f ? 0u : __float_as_uint(x);
-  const unsigned key = (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+  // x + 0 maps -0 to +0 and is x otherwise (NaN aside); flipping every bit of a negative value
+  // and the sign bit of a positive one orders the bit patterns like the floats
+  const unsigned bits = __float_as_uint(x + 0.0f);
+  const unsigned key = bits ^ ((unsigned)((int)bits >> 31) | 0x80000000u);
   return x != x ? 1u : key;
 }
 

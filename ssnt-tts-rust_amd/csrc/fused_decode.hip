@@ -207,6 +207,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     bool overrun, last, exact;
   };
   const bool tmode = a.test_mode;
+  const int o_int = (int)O;  // the final total is compared as `next_total == output_length as i32`
   auto band_of = [&](int s) {
     Band r;
     const float diagonal = o_over_i * (float)(s + 1);
@@ -225,11 +226,17 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   // steps; step s reads its own with three v_readlane instead of ~22 instructions of f32 band
   // arithmetic per step
   int bl_lb = 0, bl_ub = 0, bl_fl = 0;
+  // The overrun and exact-length rules are folded into the range as well: an overrunning step
+  // admits no total (an empty range), and an exact last step admits only O within the band.
   auto band_block = [&](int s0) {
     const Band r = band_of(s0 + lane);
-    bl_lb = r.lb;
-    bl_ub = r.ub;
-    bl_fl = (r.overrun ? 1 : 0) | (r.last ? 2 : 0) | (r.exact ? 4 : 0);
+    int lb = r.exact ? max(r.lb, o_int) : r.lb;
+    int ub = r.exact ? min(r.ub, o_int) : r.ub;
+    lb = r.overrun ? 2147483647 : lb;
+    ub = r.overrun ? (-2147483647 - 1) : ub;
+    bl_lb = lb;
+    bl_ub = ub;
+    bl_fl = r.last ? 2 : 0;
   };
   auto band_at = [&](int s) {
     const int l = s & 63;
@@ -237,12 +244,11 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     r.lb = readlane_i(bl_lb, l);
     r.ub = readlane_i(bl_ub, l);
     const int fl = readlane_i(bl_fl, l);
-    r.overrun = (fl & 1) != 0;
+    r.overrun = false;  // (folded into the range)
     r.last = (fl & 2) != 0;
-    r.exact = (fl & 4) != 0;
+    r.exact = false;
     return r;
   };
-  const int o_int = (int)O;  // the final total is compared as `next_total == output_length as i32`
   // the class rule of decode_beam_at (src/v2.rs:127-133), a per-lane constant
   const bool class_ok = a.allow_skip || i != sid;
 
@@ -351,8 +357,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       // uniform per step
       // the else-if chain of decode_beam_at as one conjunction (test_mode folded into the band),
       // bitwise so that no term becomes an exec-mask branch
-      const bool ok = (tot >= band.lb) & (tot <= band.ub) & !band.overrun &
-                      (!band.exact | (tot == o_int)) & class_ok;
+      const bool ok = (tot >= band.lb) & (tot <= band.ub) & class_ok;  // (rules folded into the range)
       const bool f = ok & band.last;
       valid = ok; code = i; lp = hist + row[0];
       nt = f ? bt : bt + 1; nu = f ? bu : bu + 1; fin = f;
