@@ -327,8 +327,21 @@ __device__ __forceinline__ void f4_sweep(const V2FwdBwdArgs& a, unsigned char* s
   // address arithmetic per cell)
   const __amdgpu_buffer_rsrc_t ws_r = __builtin_amdgcn_make_buffer_rsrc(
       ws, (short)0, (int)((size_t)(Imax + 1) * Wc * sizeof(xf)), 0x00020000);
+  // the windows of 64 consecutive steps, one per lane (lane l: the row of step 64 j + l), formed
+  // once per block; a step reads the next step's window with two v_readlane instead of the
+  // f32 band arithmetic and its branches (the same rule, f4_window, evaluated per lane)
+  int wlo = 0, whi = 0;
+  auto win_block = [&](int k0) {
+    const int kk = k0 + lane;
+    f4_window(u, FWD ? kk : I - kk, wlo, whi);
+  };
+  auto win_at = [&](int kk, int& l, int& h) {
+    l = __builtin_amdgcn_readlane(wlo, kk & 63);
+    h = __builtin_amdgcn_readlane(whi, kk & 63);
+  };
+  win_block(0);
   int lo, hi;  // window of the row the next step produces (formed before the barrier)
-  f4_window(u, FWD ? 1 : I - 1, lo, hi);
+  win_at(1, lo, hi);
   // step k (1..I) produces row r = k (alpha) / I - k (beta) from the row of step k - 1 with the
   // class weights of sweep step k - 1; false: a window beyond the row capacity (reported)
   auto step = [&](int k) {
@@ -372,7 +385,10 @@ __device__ __forceinline__ void f4_sweep(const V2FwdBwdArgs& a, unsigned char* s
     if (zi >= 0 && zi < nz) dst[max(hi - lo + 1, 0) + zi] = xf_zero();
     plo = lo;
     phi = hi;
-    if (k < I) f4_window(u, FWD ? k + 1 : I - k - 1, lo, hi);  // (before the barrier)
+    if (k < I) {  // (before the barrier)
+      if (((k + 1) & 63) == 0) win_block(k + 1);
+      win_at(k + 1, lo, hi);
+    }
     lds_sync();
     if (la) f4_log_row(la + (size_t)r * X, dst, plo, phi, X);
     return true;
