@@ -455,12 +455,18 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
   }
 }
 
-constexpr int kF4GradThreads = 256;
-constexpr int kF4GradWaves = kF4GradThreads / 64;
+// threads of a gradient workgroup: one wave up to 16 classes (a workgroup's time is its chain of
+// dependent global loads, so more, smaller workgroups per CU overlap more of them: 64 threads
+// 75 us, 128 87 us, 256 102 us at configs[4]), then more waves so a wave's class partials stay
+// within its registers
+template <int DC>
+constexpr int f4_grad_threads() { return DC <= 16 ? 64 : DC <= 32 ? 128 : 256; }
 
 // gradients of step t = blockIdx.y (and the debug beta row t); rows t >= I: zeros / -inf
 template <int DC>
-__global__ __launch_bounds__(kF4GradThreads) void k_f4_grad(V2FwdBwdArgs a) {
+__global__ __launch_bounds__(f4_grad_threads<DC>()) void k_f4_grad(V2FwdBwdArgs a) {
+  constexpr int kF4GradThreads = f4_grad_threads<DC>();
+  constexpr int kF4GradWaves = kF4GradThreads / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x, t = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -556,7 +562,7 @@ int launch_f4(const V2FwdBwdArgs& a, size_t lds, size_t glds, hipStream_t st) {
   if (glds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_f4_grad<DC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds);
-  hipLaunchKernelGGL(k_f4_grad<DC>, dim3(a.B, a.Imax + 1), dim3(kF4GradThreads), glds, st, a);
+  hipLaunchKernelGGL(k_f4_grad<DC>, dim3(a.B, a.Imax + 1), dim3(f4_grad_threads<DC>()), glds, st, a);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
