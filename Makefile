@@ -17,8 +17,8 @@ HIPFLAGS  := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisi
 HIP_SRCS  := $(CSRC)/fwd_bwd.hip $(CSRC)/fwd_bwd_stream.hip $(CSRC)/fwd_bwd_wide.hip $(CSRC)/v2_fwd_bwd.hip \
              $(CSRC)/decode.hip \
              $(CSRC)/fused_decode.hip $(CSRC)/capi.hip
-# the A/B build adds the kernels only its knobs reach (the pair kernel)
-AB_SRCS   := $(HIP_SRCS) $(CSRC)/fwd_bwd_pair.hip $(CSRC)/fwd_bwd_rows.hip
+# the A/B and diagnostic builds compile the same sources with their own macros
+AB_SRCS   := $(HIP_SRCS)
 HIP_HDRS  := $(wildcard $(CSRC)/*.h) include/ssnt_tts_c.h
 HIP_OBJS  := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(HIP_SRCS))
 
@@ -28,7 +28,7 @@ lib: $(LIB)
 oracle: $(ORACLE)
 
 # A/B build (tests and tools only; include/ssnt_tts_c_ab.h): the product plus process-wide kernel
-# / staging / sync knobs, the pair kernel and the selection decode ordering. Own soname, so a
+# / staging / sync knobs and the selection decode ordering. Own soname, so a
 # process can load it beside the product library.
 ABDIR     := $(LIBDIR)/ab
 AB_OBJS   := $(patsubst $(CSRC)/%.hip,$(ABDIR)/obj/%.o,$(AB_SRCS))
@@ -67,43 +67,6 @@ $(DFDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
 $(DFDIR)/libssnt_tts_c.so: $(DF_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(DF_OBJS) -Wl,-soname,libssnt_tts_c.so
 
-# experiment build: one kernel instance (K=2, no log_obs), diag stamps, SSNT_EXP env knobs
-EXPDIR    := $(LIBDIR)/exp
-EXP_OBJS  := $(patsubst $(CSRC)/%.hip,$(EXPDIR)/obj/%.o,$(AB_SRCS))
-lib-exp: $(EXPDIR)/libssnt_tts_c.so
-$(EXPDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
-	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -DSSNT_AB -DSSNT_DIAG -DSSNT_EXP -c $< -o $@
-# experiment build without the diagnostic stamps (kernel time of SSNT_EXP masks, tools/ab_exp.py)
-EXPNDIR   := $(LIBDIR)/expnd
-EXPN_OBJS := $(patsubst $(CSRC)/%.hip,$(EXPNDIR)/obj/%.o,$(AB_SRCS))
-lib-expnd: $(EXPNDIR)/libssnt_tts_c.so
-$(EXPNDIR)/obj/%.o: $(CSRC)/%.hip $(HIP_HDRS)
-	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -DSSNT_AB -DSSNT_EXP -c $< -o $@
-$(EXPNDIR)/libssnt_tts_c.so: $(EXPN_OBJS)
-	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(EXPN_OBJS) -Wl,-soname,libssnt_tts_c.so
-
-$(EXPDIR)/libssnt_tts_c.so: $(EXP_OBJS)
-	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(EXP_OBJS) -Wl,-soname,libssnt_tts_c.so
-
-# study builds of the reverted per-utterance-descriptor streaming kernel: the
-# product objects with fwd_bwd_stream.o rebuilt -DSSNT_VAR_DESC (register soffset on the wide
-# stores: LLVM inserts no store-data wait states -> wrong gradients on gfx950), and the same with
-# the two wait states put back (-DSSNT_VAR_DESC_NOP). Never the product.
-OTHER_OBJS := $(filter-out $(LIBDIR)/obj/fwd_bwd_stream.o,$(HIP_OBJS))
-lib-var-desc: $(LIBDIR)/var_desc/libssnt_tts_c.so $(LIBDIR)/var_desc_nop/libssnt_tts_c.so
-$(LIBDIR)/var_desc/fwd_bwd_stream.o: $(CSRC)/fwd_bwd_stream.hip $(HIP_HDRS)
-	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -DSSNT_VAR_DESC -c $< -o $@
-$(LIBDIR)/var_desc_nop/fwd_bwd_stream.o: $(CSRC)/fwd_bwd_stream.hip $(HIP_HDRS)
-	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -DSSNT_VAR_DESC -DSSNT_VAR_DESC_NOP -c $< -o $@
-$(LIBDIR)/var_desc/libssnt_tts_c.so: $(LIBDIR)/var_desc/fwd_bwd_stream.o $(OTHER_OBJS)
-	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^ -Wl,-soname,libssnt_tts_c.so
-$(LIBDIR)/var_desc_nop/libssnt_tts_c.so: $(LIBDIR)/var_desc_nop/fwd_bwd_stream.o $(OTHER_OBJS)
-	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^ -Wl,-soname,libssnt_tts_c.so
-
 $(ORACLE): oracle/ssnt_oracle.c
 	@mkdir -p $(dir $@)
 	gcc -O3 -std=c11 -fopenmp -ffp-contract=off -fPIC -shared -Wall -o $@ $< -lm
@@ -111,4 +74,4 @@ $(ORACLE): oracle/ssnt_oracle.c
 clean:
 	rm -rf $(LIBDIR) oracle/build
 
-.PHONY: all lib lib-ab lib-diag lib-diag-fault lib-exp lib-expnd lib-var-desc oracle clean
+.PHONY: all lib lib-ab lib-diag lib-diag-fault oracle clean

@@ -150,6 +150,22 @@ int ssnt_fwd_bwd_sum_device(const float *log_trans, const float *log_obs, const 
                             float *loss, float *grad_trans, float *grad_obs, float *log_alpha,
                             float *log_beta, void *workspace, size_t workspace_bytes, int *status,
                             float *loss_sum, void *sum_state, void *stream);
+/* Float64 outputs of the same computation (the north_star bar is 1e-5 abs on
+ * log-alpha / log-beta, which an f32 value cannot hold once |log alpha| > ~84 -- half an f32
+ * ulp at configs[4]'s |log alpha| ~ 2231 is 1.2e-4). The dispatched kernel writes its
+ * split-exponent state m * 2^e (m in [0.5, 1)) instead of f32 logs, and a second pass forms
+ * e*ln2 + ln(m) in float64 on the GPU: loss (B) = -ln Z, log_alpha / log_beta (B,T,U) (NULL =
+ * skip; -inf outside the lattice). grad_trans / grad_obs and every rule as
+ * ssnt_fwd_bwd_device (the same launch, the same kernel the shape dispatches; gradients
+ * bit-identical). `workspace`: ssnt_fwd_bwd_debug64_workspace_size() bytes (the plain
+ * workspace plus the state planes, 16 B per cell). Device pointers, asynchronous. New: the
+ * reference has no forward-backward. */
+size_t ssnt_fwd_bwd_debug64_workspace_size(int batch, int max_steps, int max_pos);
+int ssnt_fwd_bwd_debug64_device(const float *log_trans, const float *log_obs, const int *step_len,
+                                const int *pos_len, int batch, int max_steps, int max_pos,
+                                int flags, double *loss, float *grad_trans, float *grad_obs,
+                                double *log_alpha, double *log_beta, void *workspace,
+                                size_t workspace_bytes, int *status, void *stream);
 /* Host-pointer variant (synchronous; copies through the calling thread's GPU context). */
 int ssnt_fwd_bwd(const float *log_trans, const float *log_obs, const int *step_len,
                  const int *pos_len, int batch, int max_steps, int max_pos, int flags,

@@ -7,7 +7,7 @@
  * caller flipping one changes the kernel every other thread's next call runs. They exist to
  * force a kernel the default dispatch would not pick for a shape (parity of every kernel on
  * the same inputs) and to time alternatives. Every form they select is bit-identical to the
- * default (except the pair kernel, variant 12: its own rounding order, oracle ORACLE_PAIR).
+ * default.
  * The workspace size ssnt_fwd_bwd_workspace_size() returns holds for the knobs' values at the
  * time of the query.
  */
@@ -23,8 +23,7 @@ extern "C" {
 #endif
 
 /* forward-backward kernel: 0 default dispatch, 1 two-wave kernel, 2 segmented kernel at every U
- * it takes, 12 the pair kernel first (U <= 128 without log_obs); env SSNT_FWD_BWD_KERNEL=simple
- * selects 1 at first use */
+ * it takes; env SSNT_FWD_BWD_KERNEL=simple selects 1 at first use */
 int ssnt_fwd_bwd_set_variant(int variant);
 /* segmented kernel: positions per lane (1 or 2) and the workgroup split (-1 auto, 0, 1) */
 int ssnt_fwd_bwd_wide_lanes(int k);
@@ -38,7 +37,7 @@ int ssnt_fused_decode_select(int mode);
 int ssnt_set_host_staging(int mode);
 int ssnt_set_host_sync(int mode);
 /* diagnostics: per-phase clock of the per-step symbols, empty-kernel launch + sync floor, and the
- * in-kernel stamps of the diagnostic builds (make lib-diag / lib-exp; -1 elsewhere) */
+ * in-kernel stamps of the diagnostic build (make lib-diag; -1 elsewhere) */
 int ssnt_diag_step_clock(int enable, double *out);
 int ssnt_diag_null_launch(int reps, double *out);
 int ssnt_diag_read(void *host, size_t bytes);

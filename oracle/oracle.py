@@ -19,7 +19,6 @@ _lib = None
 
 FLAG_TERMINAL_EMIT = 1
 FLAG_ZERO_INFINITY = 2
-ORACLE_PAIR = 1 << 16  # oracle-only: the pair kernel's recurrence (ssnt_oracle.c)
 
 _f32p = ctypes.POINTER(ctypes.c_float)
 _f64p = ctypes.POINTER(ctypes.c_double)
@@ -233,12 +232,8 @@ def tone_lattice_decode(logits, input_length, empty_tone_id, n_threads=0):
 
 
 def fwd_bwd_xf(log_trans, step_len, pos_len, log_obs=None, flags=FLAG_TERMINAL_EMIT,
-               debug=False, n_threads=0, pair=False):
-    """Exact split-exponent f32 fwd-bwd (the arithmetic the HIP kernel reproduces bit-exactly).
-    pair=True: the pair recurrence of the pair kernel (csrc/fwd_bwd_pair.hip, no log_obs)."""
-    if pair:
-        assert log_obs is None, "the pair recurrence has no log_obs form"
-        flags = int(flags) | ORACLE_PAIR
+               debug=False, n_threads=0):
+    """Exact split-exponent f32 fwd-bwd (the arithmetic the HIP kernel reproduces bit-exactly)."""
     lt = _f32(log_trans)
     B, T, U, _ = lt.shape
     lo = None if log_obs is None else _f32(log_obs)
@@ -258,6 +253,39 @@ def fwd_bwd_xf(log_trans, step_len, pos_len, log_obs=None, flags=FLAG_TERMINAL_E
         out["log_alpha"] = la
         out["log_beta"] = lb
     return out
+
+
+XF_DTYPE = np.dtype([("m", np.float32), ("e", np.int32)])
+LN2_F64 = 0.6931471805599453
+
+
+def xf_log64(state):
+    """float64 natural log of split-exponent values {m, e}: e*ln2 + ln(m) (zeros -> -inf)."""
+    m = state["m"].astype(np.float64)
+    out = np.full(m.shape, -np.inf)
+    nz = m != 0.0
+    out[nz] = state["e"][nz].astype(np.float64) * LN2_F64 + np.log(m[nz])
+    return out
+
+
+def fwd_bwd_xf_state(log_trans, step_len, pos_len, log_obs=None, flags=FLAG_TERMINAL_EMIT,
+                     n_threads=0):
+    """The split-exponent fwd-bwd's own normalized state: alpha / beta (B,T,U) and Z (B) as
+    XF_DTYPE records (what ssnt_fwd_bwd_debug64_device forms its float64 logs from)."""
+    lt = _f32(log_trans)
+    B, T, U, _ = lt.shape
+    lo = None if log_obs is None else _f32(log_obs)
+    loss = np.zeros(B, np.float32)
+    grad = np.zeros((B, T, U, 2), np.float32)
+    al = np.zeros((B, T, U), XF_DTYPE)
+    be = np.zeros((B, T, U), XF_DTYPE)
+    z = np.zeros(B, XF_DTYPE)
+    vp = ctypes.c_void_p
+    lib().oracle_fwd_bwd_xf_state(B, T, U, _p(lt, _f32p), _p(lo, _f32p),
+                                  _p(_i32(step_len), _i32p), _p(_i32(pos_len), _i32p), int(flags),
+                                  _p(loss, _f32p), _p(grad, _f32p), vp(al.ctypes.data),
+                                  vp(be.ctypes.data), vp(z.ctypes.data), int(n_threads))
+    return dict(loss=loss, grad=grad, alpha=al, beta=be, z=z)
 
 
 def fwd_bwd_f64(log_trans, step_len, pos_len, log_obs=None, flags=FLAG_TERMINAL_EMIT):

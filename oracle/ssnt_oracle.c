@@ -611,11 +611,6 @@ int oracle_tone_lattice_decode(int B, int T, int W, int C, const float *logits,
  * ========================================================================================== */
 #define FLAG_TERMINAL_EMIT 1
 #define FLAG_ZERO_INFINITY 2
-/* internal (oracle only, never a kernel flag): the pair recurrence of the pair kernel
- * (csrc/fwd_bwd_pair.hip). Even rows advance two steps at a time, odd rows are one
- * step from the even row before them, the cut is even. No log_obs. */
-#define ORACLE_PAIR (1 << 16)
-
 /* --- split-exponent ("xf") f32 arithmetic: value = m * 2^e ------------------------------- */
 typedef struct { float m; int32_t e; } xf;
 #define XF_EZERO (-(1 << 29))
@@ -626,11 +621,14 @@ static const float L2E = 0x1.715476p+0f;
 static const float LN2HI = 0x1.62e400p-1f;  /* 0x3f317200 */
 static const float LN2LO = 0x1.7f7d1cp-20f; /* 0x35bfbe8e */
 static const float SQRTH = 0x1.6a09e6p-1f;
-/* e^r on [-ln2/2, ln2/2], deg 6. The coefficients are fixed constants of the arithmetic
- * definition (shared with csrc/xf_math.h); their accuracy against float64 exp/log is checked by
- * tests/test_oracle_fwd_bwd.py (the fit script was not kept). */
-static const float EC[7] = {0x1p+0f, 0x1p+0f, 0x1p-1f, 0x1.555404p-3f, 0x1.555464p-5f,
-                            0x1.126facp-7f, 0x1.6da758p-10f};
+/* e^r on [-ln2/2, ln2/2], deg 6, c0 = c1 = 1 and c2 = 1/2 exact, c3..c6 a relative-error minimax
+ * fit (0.06 ulp of approximation error; tools/fit_exp_poly.py). The coefficients are fixed
+ * constants of the arithmetic definition, shared with csrc/xf_math.h and csrc/lattice_dev.h.
+ * Round 5 replaced a fit whose error curve had a one-sided bias (0.33 ulp at r = -0.3): over a
+ * 2000-step lattice that bias accumulated to 1.1e-5 in log-alpha, past the north_star's 1e-5
+ * (DESIGN.md 6.1). */
+static const float EC[7] = {0x1p+0f, 0x1p+0f, 0x1p-1f, 0x1.5554a4p-3f, 0x1.555688p-5f,
+                            0x1.122f66p-7f, 0x1.6b6ep-10f};
 /* ln(1+t)/t on [sqrt(.5)-1, sqrt(2)-1], deg 8 */
 static const float LC[9] = {0x1p+0f,         -0x1.fffff8p-2f, 0x1.55579p-2f,
                             -0x1.0005a6p-2f, 0x1.98b80ap-3f,  -0x1.5329bep-3f,
@@ -678,73 +676,10 @@ static inline xf xf_add(float ma, int32_t ea, float mb, int32_t eb) {
 
 static inline float xf_neg_post(float m, int32_t e) { return 0.0f - ldexpf(m, e); }
 
-/* ---- pair recurrence (ORACLE_PAIR; csrc/fwd_bwd_pair.hip) ------------------------------------
- * Two steps of the emit/shift recurrence composed into one: with factors E, Sh of rows s and
- * s+1 (primed), alpha[s+2][p] = c0 a[p] + c1 a[p-1] + c2 a[p-2] (a = alpha[s]) and
- * beta[s][p] = d0 b[p] + d1 b[p+1] + d2 b[p+2] (b = beta[s+2]), where
- *   c0 = E E'              c1 = Sh[p-1] E'[p] (+) E[p-1] Sh'[p-1]    c2 = Sh[p-2] Sh'[p-1]
- *   d0 = E E'              d1 = E[p] Sh'[p] (+) Sh[p] E'[p+1]        d2 = Sh[p] Sh'[p+1]
- * (products unnormalized, (+) = xf_add). The three terms are summed in order (t0 + t1) + t2
- * after aligning to the exponent max clamped at XF_EZERO, then normalized. */
-static const xf XF_Z = {0.0f, XF_EZERO};
-static inline xf xf_mul(xf a, xf b) { return (xf){a.m * b.m, a.e + b.e}; }
-static inline xf xf_sum3(xf t0, xf t1, xf t2) {
-    int32_t em = t0.e > t1.e ? t0.e : t1.e;
-    em = em > t2.e ? em : t2.e;
-    em = em > XF_EZERO ? em : XF_EZERO;
-    const float s = (ldexpf(t0.m, t0.e - em) + ldexpf(t1.m, t1.e - em)) + ldexpf(t2.m, t2.e - em);
-    return xf_norm(s, em);
-}
-/* one forward step from row s (the oracle's single-step alpha, no log_obs) */
-static void step_fwd(const xf *a, const xf *E, const xf *Sh, int U, xf *out) {
-    for (int p = 0; p < U; ++p) {
-        const float sm = a[p].m * E[p].m;
-        const int32_t se = a[p].e + E[p].e;
-        float hm = 0.0f;
-        int32_t he = XF_EZERO;
-        if (p > 0) {
-            hm = a[p - 1].m * Sh[p - 1].m;
-            he = a[p - 1].e + Sh[p - 1].e;
-        }
-        const int32_t em = se > he ? se : he;
-        out[p] = xf_norm(ldexpf(sm, se - em) + ldexpf(hm, he - em), em);
-    }
-}
-/* one backward step into row s from b = beta[s+1] */
-static void step_bwd(const xf *b, const xf *E, const xf *Sh, int U, xf *out) {
-    for (int p = 0; p < U; ++p) {
-        const xf q = b[p], r = (p + 1 < U) ? b[p + 1] : XF_Z;
-        out[p] = xf_add(E[p].m * q.m, E[p].e + q.e, Sh[p].m * r.m, Sh[p].e + r.e);
-    }
-}
-static void pair_fwd(const xf *a, const xf *E, const xf *Sh, const xf *E1, const xf *Sh1, int U, xf *out) {
-    for (int p = 0; p < U; ++p) {
-        const xf c0 = xf_mul(E[p], E1[p]);
-        xf c1 = XF_Z, c2 = XF_Z;
-        if (p >= 1) {
-            const xf ta = xf_mul(Sh[p - 1], E1[p]), tb = xf_mul(E[p - 1], Sh1[p - 1]);
-            c1 = xf_add(ta.m, ta.e, tb.m, tb.e);
-        }
-        if (p >= 2) c2 = xf_mul(Sh[p - 2], Sh1[p - 1]);
-        out[p] = xf_sum3(xf_mul(a[p], c0), p >= 1 ? xf_mul(a[p - 1], c1) : XF_Z,
-                         p >= 2 ? xf_mul(a[p - 2], c2) : XF_Z);
-    }
-}
-static void pair_bwd(const xf *b, const xf *E, const xf *Sh, const xf *E1, const xf *Sh1, int U, xf *out) {
-    for (int p = 0; p < U; ++p) {
-        const xf d0 = xf_mul(E[p], E1[p]);
-        const xf ta = xf_mul(E[p], Sh1[p]);
-        const xf tb = (p + 1 < U) ? xf_mul(Sh[p], E1[p + 1]) : XF_Z;
-        const xf d1 = xf_add(ta.m, ta.e, tb.m, tb.e);
-        const xf d2 = (p + 1 < U) ? xf_mul(Sh[p], Sh1[p + 1]) : XF_Z;
-        out[p] = xf_sum3(xf_mul(b[p], d0), (p + 1 < U) ? xf_mul(b[p + 1], d1) : XF_Z,
-                         (p + 2 < U) ? xf_mul(b[p + 2], d2) : XF_Z);
-    }
-}
 
 static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S, int P,
                            int flags, float *loss, float *g, float *go, float *la, float *lb,
-                           xf *A, xf *Bt, xf *E, xf *Sh, xf *O) {
+                           xf *A, xf *Bt, xf *E, xf *Sh, xf *O, xf *st_a, xf *st_b, xf *st_z) {
     const bool term = (flags & FLAG_TERMINAL_EMIT) != 0;
     const size_t TU = (size_t)T * U;
     /* zero / -inf fill of every output cell (cells outside (S,P) keep these). */
@@ -752,6 +687,9 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
     if (go) memset(go, 0, sizeof(float) * TU);
     for (size_t i = 0; la && i < TU; ++i) la[i] = -INFINITY;
     for (size_t i = 0; lb && i < TU; ++i) lb[i] = -INFINITY;
+    for (size_t i = 0; st_a && i < TU; ++i) st_a[i] = (xf){0.0f, XF_EZERO};
+    for (size_t i = 0; st_b && i < TU; ++i) st_b[i] = (xf){0.0f, XF_EZERO};
+    if (st_z) *st_z = (xf){0.0f, XF_EZERO};
     const bool feasible = S >= 1 && P >= 1 && S <= T && P <= U && S >= P;
     if (!feasible) {
         *loss = (flags & FLAG_ZERO_INFINITY) ? 0.0f : INFINITY;
@@ -765,19 +703,10 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
             Sh[c] = xf_exp(lt[c * 2 + 1], p < P - 1);
             O[c] = lo ? xf_exp(lo[c], p < P) : (xf){1.0f, 0};
         }
-    const bool pair = (flags & ORACLE_PAIR) != 0 && !lo;
     /* alpha */
     for (int p = 0; p < U; ++p) A[p] = (xf){0.0f, XF_EZERO};
     A[0] = lo ? xf_norm(O[0].m, O[0].e) : (xf){0.5f, 1};
-    if (pair) {
-        for (int s = 2; s < S; s += 2)
-            pair_fwd(A + (size_t)(s - 2) * U, E + (size_t)(s - 2) * U, Sh + (size_t)(s - 2) * U,
-                     E + (size_t)(s - 1) * U, Sh + (size_t)(s - 1) * U, U, A + (size_t)s * U);
-        for (int s = 1; s < S; s += 2)
-            step_fwd(A + (size_t)(s - 1) * U, E + (size_t)(s - 1) * U, Sh + (size_t)(s - 1) * U, U,
-                     A + (size_t)s * U);
-    }
-    for (int s = 1; s < S && !pair; ++s)
+    for (int s = 1; s < S; ++s)
         for (int p = 0; p < U; ++p) {
             const xf a = A[(size_t)(s - 1) * U + p];
             const xf e = E[(size_t)(s - 1) * U + p];
@@ -807,23 +736,7 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
         const xf e = E[(size_t)(S - 1) * U + P - 1];
         Bt[(size_t)(S - 1) * U + P - 1] = term ? xf_norm(e.m, e.e) : (xf){0.5f, 1};
     }
-    if (pair) {
-        /* even rows: two steps down from the even row above, or (S-1 odd) one step from beta[S-1];
-         * odd rows below S-1: one step down from the even row above */
-        for (int s = (S - 1) & ~1; s >= 0; s -= 2) {
-            if (s == S - 1) continue;
-            xf *o = Bt + (size_t)s * U;
-            if (s + 2 <= S - 1)
-                pair_bwd(Bt + (size_t)(s + 2) * U, E + (size_t)s * U, Sh + (size_t)s * U,
-                         E + (size_t)(s + 1) * U, Sh + (size_t)(s + 1) * U, U, o);
-            else
-                step_bwd(Bt + (size_t)(s + 1) * U, E + (size_t)s * U, Sh + (size_t)s * U, U, o);
-        }
-        for (int s = 1; s < S - 1; s += 2)
-            step_bwd(Bt + (size_t)(s + 1) * U, E + (size_t)s * U, Sh + (size_t)s * U, U,
-                     Bt + (size_t)s * U);
-    }
-    for (int s = S - 2; s >= 0 && !pair; --s)
+    for (int s = S - 2; s >= 0; --s)
         for (int p = 0; p < U; ++p) {
             xf q = Bt[(size_t)(s + 1) * U + p], r = {0.0f, XF_EZERO};
             if (p + 1 < U) r = Bt[(size_t)(s + 1) * U + p + 1];
@@ -839,7 +752,7 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
             Bt[(size_t)s * U + p] = xf_add(e.m * q.m, e.e + q.e, sh.m * r.m, sh.e + r.e);
         }
     /* Z at the cut M = (S-1)>>1: binary tree (pairs (2i,2i+1) first) over p in [0, 2^n). */
-    const int M = pair ? ((S - 1) >> 1) & ~1 : (S - 1) >> 1;  /* the pair kernel's cut is even */
+    const int M = (S - 1) >> 1;
     int n2 = 1;
     while (n2 < P) n2 <<= 1;
     xf *w = (xf *)malloc(sizeof(xf) * n2);
@@ -854,6 +767,7 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
         for (int i = 0; i < len / 2; ++i) w[i] = xf_add(w[2 * i].m, w[2 * i].e, w[2 * i + 1].m, w[2 * i + 1].e);
     xf Z = (n2 == 1) ? xf_norm(w[0].m, w[0].e) : w[0];
     free(w);
+    if (st_z) *st_z = Z;
     if (Z.m == 0.0f) {
         *loss = (flags & FLAG_ZERO_INFINITY) ? 0.0f : INFINITY;
         return;
@@ -866,6 +780,8 @@ static void xf_fwd_bwd_one(const float *lt, const float *lo, int T, int U, int S
         for (int p = 0; p < P; ++p) {
             if (la) la[(size_t)s * U + p] = xf_log(A[(size_t)s * U + p]);
             if (lb) lb[(size_t)s * U + p] = xf_log(Bt[(size_t)s * U + p]);
+            if (st_a) st_a[(size_t)s * U + p] = A[(size_t)s * U + p];
+            if (st_b) st_b[(size_t)s * U + p] = Bt[(size_t)s * U + p];
         }
     /* gradients */
     for (int s = 0; s < S; ++s)
@@ -921,7 +837,38 @@ int oracle_fwd_bwd_xf(int B, int T, int U, const float *log_trans, const float *
                            pos_len[b], flags, loss + b, grad + off * 2,
                            grad_obs ? grad_obs + off : NULL, log_alpha ? log_alpha + off : NULL,
                            log_beta ? log_beta + off : NULL, buf, buf + TU, buf + 2 * TU,
-                           buf + 3 * TU, buf + 4 * TU);
+                           buf + 3 * TU, buf + 4 * TU, NULL, NULL, NULL);
+        }
+        free(buf);
+    }
+    return ORC_OK;
+}
+
+/* The same computation, returning the normalized split-exponent state itself: alpha / beta
+ * (B,T,U) and Z (B) as {m, e} pairs (m in [0.5, 1) or the zero {0, XF_EZERO}; cells outside
+ * (S,P) and rows of infeasible utterances are zeros). This is what the device debug64 entry
+ * (ssnt_fwd_bwd_debug64_device) turns into float64 logs, e*ln2 + ln(m): tests compare the GPU's
+ * state with this bit for bit and its float64 logs with oracle_fwd_bwd_f64. */
+int oracle_fwd_bwd_xf_state(int B, int T, int U, const float *log_trans, const float *log_obs,
+                            const int32_t *step_len, const int32_t *pos_len, int flags,
+                            float *loss, float *grad, void *alpha, void *beta, void *z,
+                            int n_threads) {
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel
+#endif
+    {
+        const size_t TU = (size_t)T * U;
+        xf *buf = (xf *)malloc(sizeof(xf) * TU * 5);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic)
+#endif
+        for (int b = 0; b < B; ++b) {
+            const size_t off = (size_t)b * TU;
+            xf_fwd_bwd_one(log_trans + off * 2, log_obs ? log_obs + off : NULL, T, U, step_len[b],
+                           pos_len[b], flags, loss + b, grad + off * 2, NULL, NULL, NULL, buf,
+                           buf + TU, buf + 2 * TU, buf + 3 * TU, buf + 4 * TU,
+                           (xf *)alpha + off, (xf *)beta + off, (xf *)z + b);
         }
         free(buf);
     }

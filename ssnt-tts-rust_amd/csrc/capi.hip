@@ -689,6 +689,26 @@ int ssnt_fwd_bwd_device(const float* log_trans, const float* log_obs, const int*
   return launch_fwd_bwd(a, as_stream(stream));
 }
 
+size_t ssnt_fwd_bwd_debug64_workspace_size(int batch, int max_steps, int max_pos) {
+  if (batch <= 0 || max_steps <= 0 || max_pos <= 0) return 0;
+  return fwd_bwd_debug64_workspace_bytes(batch, max_steps, max_pos);
+}
+
+int ssnt_fwd_bwd_debug64_device(const float* log_trans, const float* log_obs, const int* step_len,
+                                const int* pos_len, int batch, int max_steps, int max_pos,
+                                int flags, double* loss, float* grad_trans, float* grad_obs,
+                                double* log_alpha, double* log_beta, void* workspace,
+                                size_t workspace_bytes, int* status, void* stream) {
+  FwdBwdArgs a{};
+  a.log_trans = log_trans; a.log_obs = log_obs; a.step_len = step_len; a.pos_len = pos_len;
+  a.B = batch; a.T = max_steps; a.U = max_pos; a.flags = flags;
+  a.grad = grad_trans; a.grad_obs = grad_obs;
+  a.workspace = workspace; a.workspace_bytes = workspace_bytes; a.status = status;
+  if (!log_trans || !step_len || !pos_len) return SSNT_ERR_INVALID_ARG;
+  if (grad_obs && !log_obs) return SSNT_ERR_INVALID_ARG;
+  return launch_fwd_bwd_debug64(a, loss, log_alpha, log_beta, as_stream(stream));
+}
+
 int ssnt_fwd_bwd_sum_device(const float* log_trans, const float* log_obs, const int* step_len,
                             const int* pos_len, int batch, int max_steps, int max_pos, int flags,
                             float* loss, float* grad_trans, float* grad_obs, float* log_alpha,

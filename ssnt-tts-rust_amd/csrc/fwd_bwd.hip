@@ -49,6 +49,9 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
   float* __restrict__ go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
   float* __restrict__ la = a.log_alpha ? a.log_alpha + (size_t)b * TU : nullptr;
   float* __restrict__ lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
+  int* __restrict__ lae = (la && a.log_alpha_e) ? a.log_alpha_e + (size_t)b * TU : nullptr;
+  int* __restrict__ lbe = (lb && a.log_beta_e) ? a.log_beta_e + (size_t)b * TU : nullptr;
+  const float dbg_zero = a.log_alpha_e ? 0.0f : -__builtin_inff();  // raw state: mantissa 0
 
   xf* cutb = reinterpret_cast<xf*>(smem);  // 64*K beta[M] slots
   xf* zsh = cutb + 64 * K;                 // Z broadcast (+ pad)
@@ -61,7 +64,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
         z[j] = 0.0f;
-        ninf[j] = -__builtin_inff();
+        ninf[j] = dbg_zero;
       }
       if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, z, z, U, lane);
       if (go) store_f_row<K, VEC>(go + (size_t)s * U, z, U, lane);
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
       }
     }
     store_row<K, VEC>(rows, X, U, lane);
-    if (la) store_log_row<K, VEC>(la, X, U, lane);
+    if (la) store_dbg_row<K, VEC>(la, lae, X, U, lane);
   }
   const int r0 = fwd ? 0 : 1;               // bwd consumes stream slot 0 for its init
   const int r1 = fwd ? M : S - M;           // phase-1 end (exclusive)
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
     const int s = S - 1;
     if (s > M) store_row<K, VEC>(rows + (size_t)s * U, X, U, lane);
     else store_row<K, VEC>(cutb, X, 64 * K, lane);
-    if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
+    if (lb) store_dbg_row<K, VEC>(lb + (size_t)s * U, lbe ? lbe + (size_t)s * U : nullptr, X, U, lane);
   }
   // ---------------- phase 1 ----------------
   for (int base = (r0 / kRing) * kRing; base < r1; base += kRing) {
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
           XRow<K> stay, shft;
           alpha_step<K, OBS>(X, E, Sh, O, stay, shft);
           store_row<K, VEC>(rows + (size_t)(r + 1) * U, X, U, lane);
-          if (la) store_log_row<K, VEC>(la + (size_t)(r + 1) * U, X, U, lane);
+          if (la) store_dbg_row<K, VEC>(la + (size_t)(r + 1) * U, lae ? lae + (size_t)(r + 1) * U : nullptr, X, U, lane);
         } else {  // beta[s], s = S-1-r
           const int s = S - 1 - r;
           XRow<K> Q, R;
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
           beta_step<K>(X, E, Sh, Q, R);
           if (s > M) store_row<K, VEC>(rows + (size_t)s * U, X, U, lane);
           else store_row<K, VEC>(cutb, X, 64 * K, lane);
-          if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
+          if (lb) store_dbg_row<K, VEC>(lb + (size_t)s * U, lbe ? lbe + (size_t)s * U : nullptr, X, U, lane);
         }
       }
     }
@@ -201,7 +204,13 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
     if (threadIdx.x == 0) a.loss[b] = inf_loss;
     return;
   }
-  if (fwd && lane == 0) a.loss[b] = 0.0f - xf_log(Z);
+  if (fwd && lane == 0) {
+    a.loss[b] = 0.0f - xf_log(Z);
+    if (a.z_state) {
+      a.z_state[2 * b] = Z.m;
+      a.z_state[2 * b + 1] = __builtin_bit_cast(float, Z.e);
+    }
+  }
   const float izm = 1.0f / Z.m;
   const int ize = -Z.e;
   // ---------------- phase 2 ----------------
@@ -256,7 +265,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
           }
           if (s + 1 < S) {
             X = Xn;
-            if (la) store_log_row<K, VEC>(la + (size_t)(s + 1) * U, X, U, lane);
+            if (la) store_dbg_row<K, VEC>(la + (size_t)(s + 1) * U, lae ? lae + (size_t)(s + 1) * U : nullptr, X, U, lane);
           }
         } else {
           const int s = S - 1 - r;  // transition s: beta[s+1] (X) -> beta[s]
@@ -276,7 +285,7 @@ __global__ __launch_bounds__(128) void k_fwd_bwd(FwdBwdArgs a) {
             if (go) store_f_row<K, VEC>(go + (size_t)s * U, gob, U, lane);
           }
           if (g) store_grad_row<K, VEC>(g + (size_t)s * U * 2, ge, gs, U, lane);
-          if (lb) store_log_row<K, VEC>(lb + (size_t)s * U, X, U, lane);
+          if (lb) store_dbg_row<K, VEC>(lb + (size_t)s * U, lbe ? lbe + (size_t)s * U : nullptr, X, U, lane);
         }
       }
     }
@@ -326,11 +335,9 @@ int launch_simple(const FwdBwdArgs& a, hipStream_t st) {
 
 // Kernel choice. The product dispatches by shape only (the streaming kernel, else the segmented
 // kernel, else the two-wave kernel). The A/B build (-DSSNT_AB, `make lib-ab`; tests and tools
-// only) adds a process-wide override: 1 two-wave kernel only, 2 segmented kernel, 3 the pair
-// kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs; its own rounding order, oracle
-// ORACLE_PAIR; measured slower: DESIGN.md 5.1a), 4 / 5 the rows kernel first (fwd_bwd_rows.hip,
-// dense / row-layout converters; bit-exact, measured slower: DESIGN.md 5.1c);
-// SSNT_FWD_BWD_KERNEL=simple selects 1 there.
+// only) adds a process-wide override: 1 two-wave kernel only, 2 segmented kernel;
+// SSNT_FWD_BWD_KERNEL=simple selects 1 there. (The pair and rows kernels of rounds 2-4, both
+// bit-exact and measured slower -- DESIGN.md 5.1a / 5.1c -- were retired to git history.)
 #ifdef SSNT_AB
 std::atomic<int> g_variant{0};
 std::once_flag g_variant_env;
@@ -383,17 +390,10 @@ size_t fwd_bwd_workspace_bytes(int B, int T, int U) {
 
 #ifdef SSNT_AB
 int set_fwd_bwd_variant(int v) {
-  // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel at every U it takes; 3..11
-  // (SSNT_EXP builds only): streaming kernel with another wave mix / ring / publication period;
-  // 12: the pair kernel first (fwd_bwd_pair.hip, U <= 128 without log_obs); 13 / 14: the rows
-  // kernel first (fwd_bwd_rows.hip, U <= 128 without log_obs; dense / row-layout converters)
-  if (v < 0 || v > 14) return SSNT_ERR_INVALID_ARG;
-#ifndef SSNT_EXP
-  if (v >= 3 && v < 12) return SSNT_ERR_UNSUPPORTED;
-#endif
+  // 0 default dispatch, 1 two-wave kernel, 2 segmented kernel at every U it takes
+  if (v < 0 || v > 2) return SSNT_ERR_INVALID_ARG;
   variant();  // the environment is read once, before any explicit choice
-  g_variant.store(v == 12 ? 3 : v == 13 ? 4 : v == 14 ? 5 : v >= 3 ? 0 : v);
-  set_stream_mix(v >= 3 && v < 12 ? v - 2 : 0);
+  g_variant.store(v);
   return SSNT_OK;
 }
 #endif
@@ -406,19 +406,10 @@ __global__ __launch_bounds__(64) void k_loss_sum(const float* loss, int B, float
 
 int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
   summed = false;
-  if (variant() == 0 || variant() == 3 || variant() == 4 || variant() == 5) {
+  if (variant() == 0) {
     FwdBwdArgs x = a;
-#ifdef SSNT_EXP
-    const char* ee = getenv("SSNT_EXP");
-    x.exp = ee ? atoi(ee) : 0;
-#endif
     if (!a.sum_state) x.loss_sum = nullptr;
-    int rc = SSNT_ERR_UNSUPPORTED;
-#ifdef SSNT_AB
-    if (variant() == 3 && stream_ring() == 0) rc = launch_fwd_bwd_pair(x, st);
-    if ((variant() == 4 || variant() == 5) && stream_ring() == 0) rc = launch_fwd_bwd_rows(x, st, variant() == 4);
-#endif
-    if (rc == SSNT_ERR_UNSUPPORTED) rc = launch_fwd_bwd_stream(x, st);
+    int rc = launch_fwd_bwd_stream(x, st);
     summed = x.loss_sum != nullptr;
     if (rc != SSNT_ERR_UNSUPPORTED) return rc;
     summed = false;
@@ -437,6 +428,73 @@ int launch_variant(const FwdBwdArgs& a, hipStream_t st, bool& summed) {
   return a.log_obs ? launch_simple<true>(x, st) : launch_simple<false>(x, st);
 }
 }  // namespace
+
+// ---- float64 debug outputs (ssnt_fwd_bwd_debug64_device) -------------------------------------
+// The kernels run in raw-state mode: mantissa / exponent planes of alpha and beta and Z per
+// utterance land in the workspace; this pass forms e*ln2 + ln(m) in float64 (zero mantissa:
+// -inf; loss: -ln Z, or the f32 kernel's +inf / 0 where Z was never formed or is 0).
+__global__ __launch_bounds__(256) void k_debug64(const float* am, const int* ae, const float* bm,
+                                                 const int* be, size_t n, double* la, double* lb,
+                                                 const float* zs, const float* loss32, int B,
+                                                 double* loss) {
+  constexpr double kLn2 = 0x1.62e42fefa39efp-1;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (la) la[i] = am[i] == 0.0f ? -__builtin_inf() : (double)ae[i] * kLn2 + log((double)am[i]);
+    if (lb) lb[i] = bm[i] == 0.0f ? -__builtin_inf() : (double)be[i] * kLn2 + log((double)bm[i]);
+  }
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)B; i += stride) {
+    const float zm = zs[2 * i];
+    const int ze = __builtin_bit_cast(int, zs[2 * i + 1]);
+    loss[i] = zm == 0.0f ? (double)loss32[i] : -((double)ze * kLn2 + log((double)zm));
+  }
+}
+
+namespace {
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace
+
+size_t fwd_bwd_debug64_workspace_bytes(int B, int T, int U) {
+  const size_t cells = (size_t)B * T * U;
+  return al256(fwd_bwd_workspace_bytes(B, T, U)) + 4 * al256(cells * 4) + al256((size_t)B * 8) +
+         al256((size_t)B * 4);
+}
+
+int launch_fwd_bwd_debug64(const FwdBwdArgs& a0, double* loss64, double* la64, double* lb64,
+                           hipStream_t st) {
+  if (a0.B < 0 || a0.T <= 0 || a0.U <= 0 || !loss64 || a0.loss_sum) return SSNT_ERR_INVALID_ARG;
+  if (a0.B == 0) return SSNT_OK;
+  const size_t need = fwd_bwd_debug64_workspace_bytes(a0.B, a0.T, a0.U);
+  if (!a0.workspace || a0.workspace_bytes < need) return SSNT_ERR_WORKSPACE;
+  const size_t cells = (size_t)a0.B * a0.T * a0.U;
+  const size_t base = fwd_bwd_workspace_bytes(a0.B, a0.T, a0.U);
+  unsigned char* w = static_cast<unsigned char*>(a0.workspace);
+  size_t off = al256(base);
+  auto take = [&](size_t bytes) { unsigned char* p = w + off; off += al256(bytes); return p; };
+  float* am = reinterpret_cast<float*>(take(cells * 4));
+  int* ae = reinterpret_cast<int*>(take(cells * 4));
+  float* bm = reinterpret_cast<float*>(take(cells * 4));
+  int* be = reinterpret_cast<int*>(take(cells * 4));
+  float* zs = reinterpret_cast<float*>(take((size_t)a0.B * 8));
+  float* l32 = reinterpret_cast<float*>(take((size_t)a0.B * 4));
+  FwdBwdArgs a = a0;
+  a.workspace = base ? a0.workspace : nullptr;  // the product dispatch sees the plain call's workspace
+  a.workspace_bytes = base;
+  a.loss = l32;
+  a.log_alpha = am;
+  a.log_beta = bm;
+  a.log_alpha_e = ae;
+  a.log_beta_e = be;
+  a.z_state = zs;
+  if (hipMemsetAsync(zs, 0, (size_t)a.B * 8, st) != hipSuccess) return SSNT_ERR_HIP;
+  int rc = launch_fwd_bwd(a, st);
+  if (rc != SSNT_OK) return rc;
+  const size_t n = la64 || lb64 ? cells : 0;
+  const int blocks = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 + 1 : 4096);
+  hipLaunchKernelGGL(k_debug64, dim3(blocks), dim3(256), 0, st, am, ae, bm, be, n, la64, lb64, zs,
+                     l32, a.B, loss64);
+  return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
+}
 
 size_t fwd_bwd_sum_state_bytes(int B) { return kSumGranuleOffset + 8 * (size_t)(B > 0 ? B : 0); }
 

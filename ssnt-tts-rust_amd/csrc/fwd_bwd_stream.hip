@@ -55,82 +55,14 @@ template <bool OBS>
 constexpr int out_slots() { return OBS ? 4 : 8; }  // chain-row ring (rows past the cut) per direction
 template <bool OBS>
 constexpr int kChainPrefetch(int R) { return R >= 16 ? 4 : 2; }  // factor rows in flight per chain
-// build-time tuning overrides (tools/build_variants.sh; the product uses the defaults)
-#ifndef SSNT_T_CDEPTH
-#define SSNT_T_CDEPTH 8
-#endif
-#ifndef SSNT_T_CPRIO
-#define SSNT_T_CPRIO 0
-#endif
-#ifndef SSNT_T_NC
-#define SSNT_T_NC 3
-#endif
-#ifndef SSNT_T_NH
-#define SSNT_T_NH 4
-#endif
 template <int K>
-constexpr int conv_depth() { return K <= 2 ? SSNT_T_CDEPTH : (K <= 4 ? 4 : 2); }  // converter prefetch rows
-
-// experiment knobs (SSNT_EXP builds only; compiled out of the product)
-#if defined(SSNT_EXP) && defined(SSNT_EXP_FIXED)
-#define EXP(bit) (((SSNT_EXP_FIXED) >> (bit)) & 1)  // one mask baked in (tools/build_fixed.sh)
-#define EXPC(bit) ((((SSNT_EXP_FIXED) >> (bit)) & 1) != 0)  // compile-time knobs (fixed builds)
-#elif defined(SSNT_EXP)
-#define EXP(bit) ((a.exp >> (bit)) & 1)
-#else
-#define EXP(bit) false
-#endif
-#ifndef EXPC
-#define EXPC(bit) false
-#endif
-
-// Timing experiment 13 (SSNT_EXP builds only, wrong results): the chains advance two rows per
-// dependent step with a three-term recurrence x[s+2][p] = c0 x[p] + c1 x[p-1] + c2 x[p-2]
-// (beta: p+1, p+2), the coefficients standing in for the step-pair products a converter would
-// form. Measures what halving the chain's dependent steps is worth before building it.
-template <int K, bool NORM>
-__device__ __forceinline__ void chain3(XRow<K>& A, const XRow<K>& C0, const XRow<K>& C1,
-                                       const XRow<K>& C2, bool fwd) {
-  float m1[K], m2[K];
-  int e1[K], e2[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    if (fwd) {
-      const int j1 = j - 1, j2 = j - 2;
-      m1[j] = (j1 >= 0) ? A.m[j1] : shr_z(A.m[K + j1]);
-      e1[j] = (j1 >= 0) ? A.e[j1] : shr_z(A.e[K + j1]);
-      m2[j] = (j2 >= 0) ? A.m[j2] : shr_z(A.m[(K + j2) % K]);
-      e2[j] = (j2 >= 0) ? A.e[j2] : shr_z(A.e[(K + j2) % K]);
-    } else {
-      const int j1 = j + 1, j2 = j + 2;
-      m1[j] = (j1 < K) ? A.m[j1] : shl_z(A.m[j1 - K]);
-      e1[j] = (j1 < K) ? A.e[j1] : shl_z(A.e[j1 - K]);
-      m2[j] = (j2 < K) ? A.m[j2] : shl_z(A.m[(j2 - K) % K]);
-      e2[j] = (j2 < K) ? A.e[j2] : shl_z(A.e[(j2 - K) % K]);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const float t0 = A.m[j] * C0.m[j], t1 = m1[j] * C1.m[j], t2 = m2[j] * C2.m[j];
-    const int f0 = A.e[j] + C0.e[j], f1 = e1[j] + C1.e[j], f2 = e2[j] + C2.e[j];
-    const int em = max(max(max(f0, f1), f2), XF_EZERO);
-    const float s = (xldexp(t0, f0 - em) + xldexp(t1, f1 - em)) + xldexp(t2, f2 - em);
-    if constexpr (NORM) {
-      A.m[j] = xmant(s);
-      A.e[j] = em + xexpo(s);
-    } else {
-      A.m[j] = s;
-      A.e[j] = em;
-    }
-  }
-}
+constexpr int conv_depth() { return K <= 2 ? 8 : (K <= 4 ? 4 : 2); }  // converter prefetch rows
 
 template <int K, bool OBS, bool LDS, int kNC, int kNH, int kRingSel, bool NV>
 __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream(FwdBwdArgs a) {
   constexpr int kWaves = 2 + 2 * kNC + 2 * kNH;
-  // kRingSel: ring slots (0 = default); tuning variants: +100 publish every step past the cut,
-  // +200 every 2 steps before it
-  constexpr int R = (kRingSel % 100) ? (kRingSel % 100) : in_slots<OBS>();
+  // kRingSel: ring slots (0 = default; 16 / 32: the A/B build's deep rings)
+  constexpr int R = kRingSel ? kRingSel : in_slots<OBS>();
   constexpr int kR2 = out_slots<OBS>() < R ? out_slots<OBS>() : R;
   static_assert(R % kR2 == 0, "ring sizes");
 #ifdef SSNT_DIAG
@@ -153,6 +85,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   float* go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
   float* la = a.log_alpha ? a.log_alpha + (size_t)b * TU : nullptr;
   float* lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
+  int* lae = (la && a.log_alpha_e) ? a.log_alpha_e + (size_t)b * TU : nullptr;  // raw-state debug
+  int* lbe = (lb && a.log_beta_e) ? a.log_beta_e + (size_t)b * TU : nullptr;
   const int p0 = K * lane;
   const bool act = p0 < U;
   const int pr = act ? p0 : Up - K;  // LDS read position (clamped for lanes past U)
@@ -168,30 +102,15 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   xf* outr = reinterpret_cast<xf*>(inr + 2 * R * slot_bytes);
   xf* rows = LDS ? outr + 2 * kR2 * Up : reinterpret_cast<xf*>(a.workspace) + (size_t)b * T * Up;
   unsigned char* junk_lane = junk + 16 * K * lane;
-#ifdef SSNT_VAR_DESC
-  // study build: one descriptor per utterance tensor, rows as scalar offsets
-  const unsigned tub8 = (unsigned)(TU * 8), tub4 = (unsigned)(TU * 4);
-  const PosOff<K, 2, NV> po8(p0, U);
-  const PosOff<K, 1, NV> po4(p0, U);
-  auto so8 = [&](int s) { return (int)((unsigned)__builtin_amdgcn_readfirstlane(s) * (unsigned)U * 8u); };
-  auto so4 = [&](int s) { return (int)((unsigned)__builtin_amdgcn_readfirstlane(s) * (unsigned)U * 4u); };
-  const __amdgpu_buffer_rsrc_t g_r = brsrc(g, g ? tub8 : 0u);
-  const __amdgpu_buffer_rsrc_t go_r = brsrc(go, go ? tub4 : 0u);
-  const __amdgpu_buffer_rsrc_t la_r = brsrc(la, la ? tub4 : 0u);
-  const __amdgpu_buffer_rsrc_t lb_r = brsrc(lb, lb ? tub4 : 0u);
-#define SSNT_GST2(v, tensor, s) gst_s<K, 2, NV>(v, tensor##_r, po8, so8(s))
-#define SSNT_GST1(v, tensor, s) gst_s<K, 1, NV>(v, tensor##_r, po4, so4(s))
-#else
 #define SSNT_GST2(v, tensor, s) gst<K, 2, NV>(v, brsrc(tensor + (size_t)(s) * U * 2, U * 8u), p0)
 #define SSNT_GST1(v, tensor, s) gst<K, 1, NV>(v, brsrc(tensor + (size_t)(s) * U, U * 4u), p0)
-#endif
 
   auto fill_rows = [&](int from, int w0, int wstep) {  // zero grads / -inf debug rows
     float z[2 * K], ninf[K];
 #pragma unroll
     for (int j = 0; j < 2 * K; ++j) z[j] = 0.0f;
 #pragma unroll
-    for (int j = 0; j < K; ++j) ninf[j] = -__builtin_inff();
+    for (int j = 0; j < K; ++j) ninf[j] = a.log_alpha_e ? 0.0f : -__builtin_inff();  // raw: mantissa 0
     for (int s = from + w0; s < T; s += wstep) {
       if (g) SSNT_GST2(z, g, s);
       if (go) SSNT_GST1(z, go, s);
@@ -255,8 +174,6 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   __syncthreads();
   Diag dg;
 
-  if (EXP(7) && role.kind != 1) return;  // experiment: converters alone
-  if (EXP(12) && role.kind != 0) return;  // experiment: chains alone (with 3, 10, 11: no waits)
   if (role.kind == 2) {
     // =============================== gradient waves ======================================
     const int d = role.d;
@@ -307,6 +224,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       if (lane == 0) {
         ctl->z = z;
         publish_loss(a, b, (z.m == 0.0f) ? inf_loss : 0.0f - xf_log(z), tag);
+        if (a.z_state) {
+          a.z_state[2 * b] = z.m;
+          a.z_state[2 * b + 1] = __builtin_bit_cast(float, z.e);
+        }
       }
       ctr_rel(&ctl->z_ready, 1);
     } else {
@@ -430,26 +351,33 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
               if constexpr (OBS) gob[q] = xf_neg_post((A.m[q] * Bs.m[q]) * izm, ae + Bs.e[q]);
             }
           }
-          if (g && !EXP(1)) SSNT_GST2(ge, g, s);
+          if (g) SSNT_GST2(ge, g, s);
           if constexpr (OBS) {
             if (go) gst<K, 1, NV>(gob, brsrc(go + (size_t)s * U, U * 4u), p0);
           }
           if (la || lb) {  // debug outputs (slow path)
-            float va[K], vb[K];
+            float va[K], vb[K], ea[K], eb[K];
 #pragma unroll
             for (int q = 0; q < K; ++q) {
-              va[q] = zero_z ? -__builtin_inff() : xf_log(xf_norm(A.m[q], A.e[q]));  // (lazy rows)
-              vb[q] = zero_z ? -__builtin_inff() : xf_log(xf_norm(Bs.m[q], Bs.e[q]));
+              const xf na = xf_norm(A.m[q], A.e[q]);  // (lazy rows)
+              const xf nb = xf_norm(Bs.m[q], Bs.e[q]);
+              const bool raw = a.log_alpha_e != nullptr;  // raw state: mantissa + exponent plane
+              va[q] = zero_z ? (raw ? 0.0f : -__builtin_inff()) : raw ? na.m : xf_log(na);
+              vb[q] = zero_z ? (raw ? 0.0f : -__builtin_inff()) : raw ? nb.m : xf_log(nb);
+              ea[q] = __builtin_bit_cast(float, na.e);
+              eb[q] = __builtin_bit_cast(float, nb.e);
             }
             if (la) gst<K, 1, NV>(va, brsrc(la + (size_t)s * U, U * 4u), p0);
             if (lb) gst<K, 1, NV>(vb, brsrc(lb + (size_t)s * U, U * 4u), p0);
+            if (lae) gst<K, 1, NV>(ea, brsrc(lae + (size_t)s * U, U * 4u), p0);
+            if (lbe) gst<K, 1, NV>(eb, brsrc(lbe + (size_t)s * U, U * 4u), p0);
           }
     };
     auto row = [&](int i, GIn& cur, GIn& nxt) {
       const bool more = i + 1 < nmine;
       const bool early = more && chain_seen >= need_of(i + 1);
       if (early) fetch(i + 1, nxt);
-      if (!EXP(0)) emit(i, cur);  // experiment: rows fetched and released, no gradient work
+      emit(i, cur);
       if (more && !early) {
         wait_chain(i + 1);
         fetch(i + 1, nxt);
@@ -473,25 +401,12 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     const int d = role.d;
     const int c = role.idx;
     constexpr int D = conv_depth<K>();
-    if (SSNT_T_CPRIO > 0) __builtin_amdgcn_s_setprio(SSNT_T_CPRIO);
     const unsigned tag0 = (d == 0 && c == 0 && b == 0 && a.loss_sum) ? sum_tag(a) : 0u;
     const int chain_end = d == 0 ? S - 1 : S;
     unsigned char* ring = inr + (size_t)d * R * slot_bytes;
-#ifdef SSNT_VAR_DESC
-    const __amdgpu_buffer_rsrc_t lt_r = brsrc(lt, tub8);
-#endif
     auto load = [&](int r, Item<K, OBS>& it) {
-      if (EXP(6)) {
-#pragma unroll
-        for (int j = 0; j < 2 * K; ++j) it.lt[j] = -0.5f - 0.01f * r;
-        return;
-      }
       const int row = min(max(d == 0 ? r : S - 1 - r, 0), T - 1);
-#ifdef SSNT_VAR_DESC
-      gld_s<K, 2, NV>(it.lt, lt_r, po8, so8(row));
-#else
       gld<K, 2, NV>(it.lt, brsrc(lt + (size_t)row * U * 2, U * 8u), p0);
-#endif
       if constexpr (OBS) {
         const int orow = min(row + 1, T - 1);
         gld<K, 1, NV>(it.ob, brsrc(lo + (size_t)orow * U, U * 4u), p0);
@@ -512,26 +427,18 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           const int r = c + kNC * k;
           const Item<K, OBS>& it = pf[i];
           XRow<K> E, Sh, O;
-          if (EXP(2)) {  // experiment: no exp() work (timing only)
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-              E.m[j] = it.lt[2 * j]; E.e[j] = 0; Sh.m[j] = it.lt[2 * j + 1]; Sh.e[j] = 0;
-              O.m[j] = 1.0f; O.e[j] = 0;
-            }
-          } else {
 #ifdef SSNT_DIAG
-            const unsigned long long tl0 = dg.now();
-            asm volatile("" :: "v"(it.lt[0]), "v"(it.lt[2 * K - 1]));  // wait for the row here
-            const unsigned long long tc0 = dg.now();
-            dg.ph[2] += tc0 - tl0;
+          const unsigned long long tl0 = dg.now();
+          asm volatile("" :: "v"(it.lt[0]), "v"(it.lt[2 * K - 1]));  // wait for the row here
+          const unsigned long long tc0 = dg.now();
+          dg.ph[2] += tc0 - tl0;
 #endif
-            convert<K, OBS>(it, P, lane, E, Sh);
-            convert_obs<K, OBS>(it, P, lane, O);
+          convert<K, OBS>(it, P, lane, E, Sh);
+          convert_obs<K, OBS>(it, P, lane, O);
 #ifdef SSNT_DIAG
-            asm volatile("" :: "v"(E.m[0]), "v"(E.e[0]), "v"(Sh.m[K - 1]), "v"(Sh.e[K - 1]));
-            dg.ph[0] += dg.now() - tc0;
+          asm volatile("" :: "v"(E.m[0]), "v"(E.e[0]), "v"(Sh.m[K - 1]), "v"(Sh.e[K - 1]));
+          dg.ph[0] += dg.now() - tc0;
 #endif
-          }
           XRow<K> Xs;
           if (d == 0) {  // L[p] = Sh[p-1]: canonical zero at p = 0
             Xs.m[0] = shr1(Sh.m[K - 1]);
@@ -546,7 +453,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           }
           // slot r % R last held row q = r - R: the chain and the gradient waves must be done
           const int q = r - R;  // (read by the chain, and by the gradient waves from row hb on)
-          if (q >= 0 && !EXP(7)) {
+          if (q >= 0) {
             const int need_c = min(q + 1, chain_end);
             if (seen_chain < need_c)
               seen_chain = spin_until<true>([&] { return ctr_ld(&ctl->sread[d]); }, need_c, a.status, dg);
@@ -568,11 +475,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           }
           // planar by element: block q holds (E, X) of positions K*l + q at 16*l -- every
           // 16-byte lane access is contiguous across the wave (no bank conflicts)
-          if (!EXP(4)) {
 #pragma unroll
-            for (int q = 0; q < K; ++q)
-              st_vec<4>(reinterpret_cast<float*>(act ? sl + (size_t)q * nl16 + 16 * lane : junk_lane + 16 * q), v + 4 * q);
-          }
+          for (int q = 0; q < K; ++q)
+            st_vec<4>(reinterpret_cast<float*>(act ? sl + (size_t)q * nl16 + 16 * lane : junk_lane + 16 * q), v + 4 * q);
           if constexpr (OBS) {
             float o[2 * K];
             xrow_pack<K>(O, o);
@@ -596,7 +501,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     fill_rows(S, d * kNC + c, 2 * kNC);  // zero the rows beyond S
     // workgroup 0 forms the batch loss sum once every utterance has published its loss (all
     // did so at their cut, long before this converter runs out of rows)
-    if (d == 0 && c == 0 && b == 0 && a.loss_sum && !EXP(7)) finish_loss_sum(a, tag0);
+    if (d == 0 && c == 0 && b == 0 && a.loss_sum) finish_loss_sum(a, tag0);
     return;
   }
 
@@ -610,11 +515,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // not what bounds it; nor do the converter polls -- with them skipped (timing experiment) a
   // step before the cut also takes ~300 cycles). All LDS
   // addresses are per-lane pointers prepared before the loop (lanes past U: junk / clamped).
-  if (!EXP(9)) __builtin_amdgcn_s_setprio(3);  // experiment 9: chains at default priority
+  __builtin_amdgcn_s_setprio(3);
   const int d = role.d;
   int ready = 0;  // stream rows known converted
   auto wait_row = [&](int r) {  // r: a row that exists
-    if (EXP(3)) return;  // experiment (timing only, wrong results): chains never poll converters
     if (r >= ready)
       ready = spin_until<false>([&] { return first_missing<kNC>(ctl->conv[d], 0); }, r + 1, a.status, dg);
   };
@@ -629,13 +533,6 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   auto rd = [&](int j, XRow<K>& E, XRow<K>& Xx, XRow<K>& O, int row = 0, bool check = false) {
     (void)row;
     (void)check;
-    if (EXP(10)) {  // experiment (timing only, wrong results): the chain reads no factors
-#pragma unroll
-      for (int q = 0; q < K; ++q) {
-        E.m[q] = 0.7f; E.e[q] = 0; Xx.m[q] = 0.6f; Xx.e[q] = -1; O.m[q] = 1.0f; O.e[q] = 0;
-      }
-      return;
-    }
     float v[4 * K];
 #pragma unroll
     for (int q = 0; q < K; ++q) ld_vec<4>(v + 4 * q, reinterpret_cast<const float*>(sptr[j] + (size_t)q * nl16));
@@ -659,7 +556,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     if (check) tag_check(&ctl->ctag[d][j], row, a.status);
 #endif
   };
-  constexpr int PF = EXPC(15) ? 4 : kChainPrefetch<OBS>(R);  // rows of factors in flight per chain
+  constexpr int PF = kChainPrefetch<OBS>(R);  // rows of factors in flight per chain
   static_assert(R % PF == 0 && PF < R, "prefetch buffers tile the ring");
   XRow<K> Eb[PF], Xb[PF], Ob[PF];
   // Steps run in half-blocks of H = R/2 (unrolled by R: slot offsets compile-time). All waits
@@ -670,8 +567,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   // Phase 2 (past the cut) publishes every H2 steps instead: there the gradient waves read each
   // factor slot right behind the chain and the converters need it back, so the hand-off
   // chain -> gradient waves -> converters -> chain has to close within the ring's slack.
-  using H1 = std::integral_constant<int, (kRingSel >= 200 ? 2 : R >= 16 ? R / 4 : R / 2)>;
-  using H2 = std::integral_constant<int, ((kRingSel >= 100 && kRingSel < 200) ? 1 : R >= 16 ? R / 8 : (R / 4 > 2 ? R / 4 : 2))>;
+  using H1 = std::integral_constant<int, (R >= 16 ? R / 4 : R / 2)>;
+  using H2 = std::integral_constant<int, (R >= 16 ? R / 8 : (R / 4 > 2 ? R / 4 : 2))>;
   auto run = [&](auto Hc, int lo, int hi, auto&& step, auto&& hwait) {
     constexpr int HS = decltype(Hc)::value;
     static_assert(R % HS == 0, "sub-blocks tile the ring");
@@ -690,10 +587,8 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           });
         }
         cbar();
-        if (!EXP(16)) {  // (experiment 16: no progress stores, timing only)
-          ctr_st(&ctl->chain[d], min(hb0 + HS, hi));
-          ctr_st(&ctl->sread[d], min(hb0 + HS, hi) + PF);  // slot reads run PF rows ahead
-        }
+        ctr_st(&ctl->chain[d], min(hb0 + HS, hi));
+        ctr_st(&ctl->sread[d], min(hb0 + HS, hi) + PF);  // slot reads run PF rows ahead
       });
     }
   };
@@ -715,7 +610,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     auto hwait = [&](int r0, int r1, bool phase2) {
       (void)r0;
       wait_row(min(r1 - 1 + PF, last));
-      if (phase2 && !EXP(11)) {  // (experiment 11: no release polls past the cut, timing only)
+      if (phase2) {
         const int q = r1 - kR2;  // newest previous occupant the half-block overwrites
         if (q > M && help_seen <= q)
           help_seen = spin_until<false>([&] { return first_missing<kNH>(ctl->help[0], M); }, q + 1, a.status, dg);
@@ -728,14 +623,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       constexpr bool phase2 = decltype(Ph)::value;
       if (!live) return;
       const int r = base + i;
-      if (EXP(13)) {
-        if constexpr (i % 2 == 0) chain3<K, (i % 4) == 2>(X, Eb[par], Xb[par], Eb[(par + 1) % PF], true);
-      } else {
-        alpha_chain<K, OBS, (i % kChainNorm) == kChainNorm - 1>(X, Eb[par], Xb[par], Ob[par]);
-      }
+      alpha_chain<K, OBS, (i % kChainNorm) == kChainNorm - 1>(X, Eb[par], Xb[par], Ob[par]);
       if constexpr (!phase2) {
         if constexpr (LDS) {
-          if (!EXP(5)) lds_xrow_st<K>(wp, X);
+          lds_xrow_st<K>(wp, X);
           wp += wstep;
         } else {
           row_st(r + 1, X);
@@ -747,7 +638,6 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 #endif
       }
       rd((i + PF) % R, Eb[par], Xb[par], Ob[par], r + PF, r + PF <= last);  // row r+PF (a stale slot past the end is dropped)
-      if (EXP(14)) cbar();  // experiment 14: the reads issue here, not sunk toward their use
     };
     if (M == 0) ctr_rel(&ctl->a_ready, 1);
     ctr_st(&ctl->sread[0], PF);  // slots of rows 0..PF-1 have been read
@@ -779,7 +669,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       constexpr int kind = decltype(Kd)::value;
       if constexpr (kind == 0) {
         if constexpr (LDS) {
-          if (!EXP(5)) lds_xrow_st<K>(wp, X);
+          lds_xrow_st<K>(wp, X);
         } else {
           row_st(S - 1 - r, X);
         }
@@ -799,7 +689,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
     auto hwait = [&](int r0, int r1, bool ring) {
       (void)r0;
       wait_row(min(r1 - 1 + PF, last));
-      if (ring && !EXP(11)) {
+      if (ring) {
         // previous occupants: stream rows up to r1-1-kR2, read by gradient rows q and q+1
         const int q = r1 - 1 - kR2;
         if (q > c && help_seen <= q + 1)
@@ -823,14 +713,9 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       constexpr int par = i % PF;
       if (!live) return;
       const int r = base + i;
-      if (EXP(13)) {
-        if constexpr (i % 2 == 0) chain3<K, (i % 4) == 2>(X, Eb[par], Xb[par], Eb[(par + 1) % PF], false);
-      } else {
-        beta_chain<K, OBS, (i % kChainNorm) == kChainNorm - 1>(X, Eb[par], Xb[par], Ob[par]);
-      }
+      beta_chain<K, OBS, (i % kChainNorm) == kChainNorm - 1>(X, Eb[par], Xb[par], Ob[par]);
       put(r, i, Kd);
       rd((i + PF) % R, Eb[par], Xb[par], Ob[par], r + PF, r + PF <= last);
-      if (EXP(14)) cbar();
     };
     cbar();
     ctr_st(&ctl->chain[1], 1);  // stream row 0 (the terminal row) is done
@@ -898,17 +783,6 @@ template <bool OBS>
 int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
   // wave mix per lane width: 16 waves (3 converters + 4 gradient waves per direction) while a
   // wave fits 128 VGPRs (K <= 2); 10 waves for K >= 4 (168 VGPRs, no spills)
-#ifdef SSNT_EXP
-  if (OBS || a.U <= 64 || a.U > 128) return SSNT_ERR_UNSUPPORTED;
-#ifdef SSNT_EXP_FIXED
-  if (a.U % 2 != 0) return SSNT_ERR_UNSUPPORTED;
-  const size_t head = stream_head_bytes(2, a.U, false, 0);
-  const size_t rows = (size_t)a.T * a.U * sizeof(xf);
-  if (head + rows > kLdsBudget) return SSNT_ERR_UNSUPPORTED;
-  return launch_stream_kernel<2, false, true, 3, 4, 0, false>(a, head + rows, st);
-#endif
-  return launch_stream_k<2, false, 3, 4>(a, st);
-#else
   if (a.U <= 64) return launch_stream_k<1, OBS, 3, 4>(a, st);
 #ifdef SSNT_AB
   if constexpr (!OBS) {  // A/B build (ssnt_fwd_bwd_stream_ring): deeper rings, rows in the workspace
@@ -917,25 +791,17 @@ int launch_stream_obs(const FwdBwdArgs& a, hipStream_t st) {
     if (a.U > 64 && a.U <= 128 && ring == 32) return launch_stream_k<2, false, 3, 4, 32>(a, st, true);
   }
 #endif
-  if (a.U <= 128) return launch_stream_k<2, OBS, SSNT_T_NC, SSNT_T_NH>(a, st);
+  if (a.U <= 128) return launch_stream_k<2, OBS, 3, 4>(a, st);
   if (a.U <= 256) return launch_stream_k<4, OBS, 2, 2>(a, st);
   // K = 8 (U <= 512, configs[4]): the two-wave kernel. The streaming kernel needs 4-slot rings to
   // fit LDS there and then ran 2.2x slower (5.7 vs 2.6 ms at B=64 T=2000 U=400).
   return SSNT_ERR_UNSUPPORTED;
-#endif
 }
 
 }  // namespace
 
-#if defined(SSNT_DIAG) && defined(SSNT_AB)
-int rows_diag_read(void* host, size_t bytes);  // fwd_bwd_rows.hip
-#endif
-
 int diag_read(void* host, size_t bytes) {
 #ifdef SSNT_DIAG
-#ifdef SSNT_AB
-  if (strncmp(last_fwd_bwd_dispatch(), "k_fwd_bwd_rows", 14) == 0) return rows_diag_read(host, bytes);
-#endif
   if (bytes > sizeof(g_diag)) bytes = sizeof(g_diag);
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess
              ? (int)bytes : -1;
@@ -947,7 +813,6 @@ int diag_read(void* host, size_t bytes) {
 }
 
 size_t stream_head_bytes(int K, int U, bool obs, int ring) {
-  ring %= 100;
   const int R = ring ? ring : obs ? in_slots<true>() : in_slots<false>();
   const int R2o = obs ? out_slots<true>() : out_slots<false>();
   const int R2 = R2o < R ? R2o : R;
@@ -957,29 +822,7 @@ size_t stream_head_bytes(int K, int U, bool obs, int ring) {
          2 * (size_t)R2 * Up * sizeof(xf);
 }
 
-#ifdef SSNT_EXP
-std::atomic<int> g_mix{0};  // tuning knob (ssnt_fwd_bwd_set_variant >= 2; SSNT_EXP builds only)
-#endif
-
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t st) {
-#if defined(SSNT_EXP) && !defined(SSNT_EXP_FIXED)
-  // tuning mixes (ssnt_fwd_bwd_set_variant >= 2): K = 2 without log_obs only, else the default
-  const int mix = g_mix.load(std::memory_order_relaxed);
-  if (mix != 0 && !a.log_obs && a.U > 64 && a.U <= 128) {
-    switch (mix) {
-      case 1: return launch_stream_k<2, false, 4, 2>(a, st);
-      case 2: return launch_stream_k<2, false, 3, 2>(a, st);
-      case 3: return launch_stream_k<2, false, 2, 4>(a, st);
-      case 4: return launch_stream_k<2, false, 2, 2>(a, st);
-      case 5: return launch_stream_k<2, false, 2, 3>(a, st);
-      case 6: return launch_stream_k<2, false, 3, 3>(a, st);
-      case 7: return launch_stream_k<2, false, 3, 4, 16>(a, st);
-      case 8: return launch_stream_k<2, false, 3, 4, 108>(a, st);
-      case 9: return launch_stream_k<2, false, 3, 4, 208>(a, st);
-      default: break;
-    }
-  }
-#endif
   return a.log_obs ? launch_stream_obs<true>(a, st) : launch_stream_obs<false>(a, st);
 }
 
@@ -991,13 +834,5 @@ int set_stream_ring(int r) {
 }
 int stream_ring() { return g_ring.load(std::memory_order_relaxed); }
 #endif
-
-void set_stream_mix(int m) {
-#ifdef SSNT_EXP
-  g_mix.store(m);
-#else
-  (void)m;
-#endif
-}
 
 }  // namespace ssnt

@@ -206,6 +206,9 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
   float* go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
   float* la = (DBG && a.log_alpha) ? a.log_alpha + (size_t)b * TU : nullptr;
   float* lb = (DBG && a.log_beta) ? a.log_beta + (size_t)b * TU : nullptr;
+  // raw-state debug mode (ssnt_fwd_bwd_debug64_device): mantissas in la / lb, exponents here
+  float* lae = (la && a.log_alpha_e) ? reinterpret_cast<float*>(a.log_alpha_e) + (size_t)b * TU : nullptr;
+  float* lbe = (lb && a.log_beta_e) ? reinterpret_cast<float*>(a.log_beta_e) + (size_t)b * TU : nullptr;
   xf* rows = gd.rows + (size_t)b * (T + 1) * U;  // row T: beta[M]
   const int p0 = kSeg * seg + K * lane;
   const unsigned rowb = (unsigned)U * 8u, rowf = (unsigned)U * 4u;
@@ -251,10 +254,16 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
     for (int j = 0; j < K; ++j) rbuf_st1(v[j], r, vo4[j], so, 0);
   };
   auto put_log = [&](float* base, int s, const XRow<K>& x, bool live = true) __attribute__((always_inline)) {
-    float v[K];
+    float v[K], ev[K];
+    float* ebase = base == la ? lae : lbe;
 #pragma unroll
-    for (int j = 0; j < K; ++j) v[j] = xf_log(xf{x.m[j], x.e[j]});
+    for (int j = 0; j < K; ++j) {
+      const xf n = xf_norm(x.m[j], x.e[j]);  // (rows are normalized: an identity)
+      v[j] = ebase ? n.m : xf_log(n);
+      ev[j] = __builtin_bit_cast(float, n.e);
+    }
     put_f(base, s, v, live);
+    if (ebase) put_f(ebase, s, ev, live);
   };
   // workspace row s (s == T: the cut row). The fields go through registers one by one: a vector
   // built straight from the adjacent fields of the row makes the compiler keep the row in memory
@@ -294,7 +303,7 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       z[j] = 0.0f;
-      ninf[j] = -__builtin_inff();
+      ninf[j] = a.log_alpha_e ? 0.0f : -__builtin_inff();  // raw state: mantissa 0
     }
     for (int s = from; s < to; ++s) {
       put_grad(s, z, z);
@@ -661,7 +670,13 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
       if (dir == 0 && part == 0 && threadIdx.x == 0) a.loss[b] = inf_loss;
       return;
     }
-    if (dir == 0 && part == 0 && threadIdx.x == 0) a.loss[b] = 0.0f - xf_log(Z);
+    if (dir == 0 && part == 0 && threadIdx.x == 0) {
+      a.loss[b] = 0.0f - xf_log(Z);
+      if (a.z_state) {
+        a.z_state[2 * b] = Z.m;
+        a.z_state[2 * b + 1] = __builtin_bit_cast(float, Z.e);
+      }
+    }
     if (!comp) {
       if (proxy) run_proxy(dir == 0 ? S - M : M);
       return;

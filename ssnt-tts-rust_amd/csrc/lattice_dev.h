@@ -209,6 +209,27 @@ __device__ __forceinline__ void store_log_row(float* __restrict__ dst, const XRo
   store_f_row<K, VEC>(dst, v, U, lane);
 }
 
+// A debug row: f32 log values, or -- raw-state mode (dst_e set, ssnt_fwd_bwd_debug64_device) --
+// the normalized mantissas into dst and the exponents into dst_e, from which the host entry forms
+// float64 logs. The same normalization xf_log starts from, so nothing is rounded on the way.
+template <int K, bool VEC>
+__device__ __forceinline__ void store_dbg_row(float* __restrict__ dst, int* __restrict__ dst_e,
+                                              const XRow<K>& r, int U, int lane) {
+  if (dst_e) {
+    float m[K], e[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const xf n = xf_norm(r.m[j], r.e[j]);
+      m[j] = n.m;
+      e[j] = __builtin_bit_cast(float, n.e);
+    }
+    store_f_row<K, VEC>(dst, m, U, lane);
+    store_f_row<K, VEC>(reinterpret_cast<float*>(dst_e), e, U, lane);
+  } else {
+    store_log_row<K, VEC>(dst, r, U, lane);
+  }
+}
+
 // exp() of the (emit, shift) pair of one position as two unnormalized xf, with packed f32
 // FMAs (v_pk_fma_f32): the same per-element IEEE operations as xf_exp (xf_math.h). Inputs are
 // clamped into [XF_LOG_MIN, XF_LOG_MAX] for the arithmetic; dead elements are zeroed at the end.
@@ -225,10 +246,10 @@ __device__ __forceinline__ void xf_exp_pair(float xe, float xs, bool ve, bool vs
   n.y = __builtin_rintf(t.y);
   f2 r = __builtin_elementwise_fma(-n, (f2){kLN2HI, kLN2HI}, x);
   r = __builtin_elementwise_fma(-n, (f2){kLN2LO, kLN2LO}, r);
-  f2 p = (f2){0x1.6da758p-10f, 0x1.6da758p-10f};
-  p = __builtin_elementwise_fma(p, r, (f2){0x1.126facp-7f, 0x1.126facp-7f});
-  p = __builtin_elementwise_fma(p, r, (f2){0x1.555464p-5f, 0x1.555464p-5f});
-  p = __builtin_elementwise_fma(p, r, (f2){0x1.555404p-3f, 0x1.555404p-3f});
+  f2 p = (f2){0x1.6b6ep-10f, 0x1.6b6ep-10f};
+  p = __builtin_elementwise_fma(p, r, (f2){0x1.122f66p-7f, 0x1.122f66p-7f});
+  p = __builtin_elementwise_fma(p, r, (f2){0x1.555688p-5f, 0x1.555688p-5f});
+  p = __builtin_elementwise_fma(p, r, (f2){0x1.5554a4p-3f, 0x1.5554a4p-3f});
   p = __builtin_elementwise_fma(p, r, (f2){0x1p-1f, 0x1p-1f});
   p = __builtin_elementwise_fma(p, r, (f2){0x1p+0f, 0x1p+0f});
   p = __builtin_elementwise_fma(p, r, (f2){0x1p+0f, 0x1p+0f});

@@ -36,14 +36,23 @@ struct FwdBwdArgs {
   int* status;  // device status word or null
   float* loss_sum;   // fixed-order sum of loss[0..B) or null
   void* sum_state;   // in-launch sum state (lattice_dev.h; zero before the first call) or null
-  int exp;      // experiment knobs (SSNT_EXP builds only; 0 in the product)
+  // raw-state debug mode (ssnt_fwd_bwd_debug64_device): with log_alpha_e / log_beta_e set, the
+  // debug rows log_alpha / log_beta receive the normalized split-exponent mantissas (0 outside
+  // the lattice) and these planes the exponents, (B,T,U); z_state (B x {m, e bits}) receives Z
+  int* log_alpha_e;
+  int* log_beta_e;
+  float* z_state;
 };
 size_t fwd_bwd_workspace_bytes(int B, int T, int U);
+// float64 debug outputs (ssnt_fwd_bwd_debug64_device): workspace bytes and the launch, which runs
+// the product dispatch in raw-state mode and then forms e*ln2 + ln(m) in float64 on the GPU
+size_t fwd_bwd_debug64_workspace_bytes(int B, int T, int U);
+int launch_fwd_bwd_debug64(const FwdBwdArgs& a, double* loss64, double* log_alpha64,
+                           double* log_beta64, hipStream_t stream);
 size_t fwd_bwd_sum_state_bytes(int B);  // 64 + 8 B
 int launch_fwd_bwd(const FwdBwdArgs& a, hipStream_t stream);
 // streaming kernel (fwd_bwd_stream.hip): SSNT_ERR_UNSUPPORTED for shapes it does not take
 int launch_fwd_bwd_stream(const FwdBwdArgs& a, hipStream_t stream);
-void set_stream_mix(int m);  // tuning only (SSNT_EXP builds)
 // segmented kernel (fwd_bwd_wide.hip): long rows (256 < U <= 1024), or any U <= 1024 when
 // any_u; SSNT_ERR_UNSUPPORTED for other shapes
 int launch_fwd_bwd_wide(const FwdBwdArgs& a, hipStream_t stream, bool any_u);
@@ -57,13 +66,6 @@ int set_stream_ring(int r);  // 0 default, 16 / 32 ring slots with workspace row
 int stream_ring();
 int set_fwd_bwd_wide_lanes(int k);  // positions per lane of the long-row kernel (1 or 2)
 int set_fwd_bwd_wide_split(int mode);  // two workgroups per direction (-1 auto, 0 off, 1 on)
-// pair kernel (fwd_bwd_pair.hip): U <= 128 without log_obs; SSNT_ERR_UNSUPPORTED otherwise
-int launch_fwd_bwd_pair(const FwdBwdArgs& a, hipStream_t stream);
-size_t pair_head_bytes(int K, int U);            // LDS bytes besides the stored rows
-size_t pair_storage_bytes(int K, int T, int U);  // stored rows of one utterance
-// rows kernel (fwd_bwd_rows.hip; U <= 128 without log_obs, U % K == 0, 16-byte aligned tensors,
-// rows within LDS): SSNT_ERR_UNSUPPORTED for shapes it does not take
-int launch_fwd_bwd_rows(const FwdBwdArgs& a, hipStream_t stream, bool dense = true);
 int set_fused_decode_select(int mode);  // -1 default, 0 full rank, 1 selection
 #else
 constexpr int stream_ring() { return 0; }

@@ -584,6 +584,9 @@ int launch_v2_fwd_bwd(const V2FwdBwdArgs& in, hipStream_t st) {
   if (lds > 160 * 1024 - 1024 || glds > 160 * 1024 - 1024) return SSNT_ERR_UNSUPPORTED;
   // (a sweep addresses one utterance's workspace rows with 32-bit offsets)
   if ((size_t)(a.Imax + 1) * a.Wcap * sizeof(xf) > 0x7fffffffu) return SSNT_ERR_UNSUPPORTED;
+  // the gradient launch reads one utterance's class log-probs through a buffer descriptor of
+  // Imax*D*4 bytes with 32-bit lane offsets: past 2 GB it would read zeros
+  if ((size_t)a.Imax * a.D * sizeof(float) > 0x7fffffffu) return SSNT_ERR_UNSUPPORTED;
   if (!a.workspace || a.workspace_bytes < v2_fwd_bwd_workspace_bytes(a.B, a.Imax, a.X - 1, a.test_mode))
     return SSNT_ERR_WORKSPACE;
   if (a.D <= 8) return launch_f4<8>(a, lds, glds, st);

@@ -59,10 +59,10 @@ __device__ __forceinline__ xf xf_exp(float x, bool valid) {
   const float n = __builtin_rintf(x * kL2E);
   float r = __builtin_fmaf(-n, kLN2HI, x);
   r = __builtin_fmaf(-n, kLN2LO, r);
-  float p = 0x1.6da758p-10f;
-  p = __builtin_fmaf(p, r, 0x1.126facp-7f);
-  p = __builtin_fmaf(p, r, 0x1.555464p-5f);
-  p = __builtin_fmaf(p, r, 0x1.555404p-3f);
+  float p = 0x1.6b6ep-10f;
+  p = __builtin_fmaf(p, r, 0x1.122f66p-7f);
+  p = __builtin_fmaf(p, r, 0x1.555688p-5f);
+  p = __builtin_fmaf(p, r, 0x1.5554a4p-3f);
   p = __builtin_fmaf(p, r, 0x1p-1f);
   p = __builtin_fmaf(p, r, 0x1p+0f);
   p = __builtin_fmaf(p, r, 0x1p+0f);

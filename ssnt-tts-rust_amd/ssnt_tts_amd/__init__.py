@@ -269,7 +269,7 @@ def _sum_state(dev, B):
 
 def ssnt_fwd_bwd(log_trans, step_len, pos_len, log_obs=None, *, terminal_emit=True,
                  zero_infinity=False, need_grad=True, debug=False, check=False, out=None,
-                 loss_sum=False):
+                 loss_sum=False, debug64=False):
     """Forward-backward over the emit/shift lattice.
 
     log_trans (B,T,U,2) f32 [emit, shift] natural-log probabilities; step_len / pos_len (B,)
@@ -279,7 +279,13 @@ def ssnt_fwd_bwd(log_trans, step_len, pos_len, log_obs=None, *, terminal_emit=Tr
     ``out`` may pass preallocated tensors under the same keys (reused, for benchmarking).
     ``loss_sum=True`` adds ``loss_sum`` (1,) = sum_b loss[b], formed inside the same launch in a
     fixed order (ssnt_fwd_bwd_sum_device).
+    ``debug64=True`` (ssnt_fwd_bwd_debug64_device) returns ``loss``, ``log_alpha`` and
+    ``log_beta`` as float64, formed on the GPU from the kernel's split-exponent state (the
+    north_star's 1e-5 bar on log-alpha / log-beta is below an f32 ulp at BASELINE magnitudes).
     """
+    if debug64:
+        return _fwd_bwd_debug64(log_trans, step_len, pos_len, log_obs, terminal_emit,
+                                zero_infinity, need_grad, check)
     lib = load(require_gpu=True)
     lt = _dev(log_trans, torch.float32, "log_trans")
     dev = lt.device
@@ -334,6 +340,38 @@ def ssnt_fwd_bwd(log_trans, step_len, pos_len, log_obs=None, *, terminal_emit=Tr
     if debug:
         res["log_alpha"] = la
         res["log_beta"] = lb
+    return res
+
+
+def _fwd_bwd_debug64(log_trans, step_len, pos_len, log_obs, terminal_emit, zero_infinity,
+                     need_grad, check):
+    lib = load(require_gpu=True)
+    lt = _dev(log_trans, torch.float32, "log_trans")
+    dev = lt.device
+    B, T, U, two = lt.shape
+    if two != 2:
+        raise ValueError("log_trans must be (B,T,U,2)")
+    sl = _dev(step_len, torch.int32, "step_len").reshape(B)
+    pl = _dev(pos_len, torch.int32, "pos_len").reshape(B)
+    lo = None if log_obs is None else _dev(log_obs, torch.float32, "log_obs").reshape(B, T, U)
+    flags = (FLAG_TERMINAL_EMIT if terminal_emit else 0) | (FLAG_ZERO_INFINITY if zero_infinity else 0)
+    loss = torch.empty((B,), dtype=torch.float64, device=dev)
+    la = torch.empty((B, T, U), dtype=torch.float64, device=dev)
+    lb = torch.empty((B, T, U), dtype=torch.float64, device=dev)
+    grad = torch.empty((B, T, U, 2), dtype=torch.float32, device=dev) if need_grad else None
+    gobs = torch.empty((B, T, U), dtype=torch.float32, device=dev) if need_grad and lo is not None else None
+    wsb = int(lib.ssnt_fwd_bwd_debug64_workspace_size(B, T, U))
+    ws = _workspace(dev, wsb)
+    st = _status(dev)
+    rc = lib.ssnt_fwd_bwd_debug64_device(_p(lt), _p(lo), _p(sl), _p(pl), B, T, U, flags, _p(loss),
+                                         _p(grad), _p(gobs), _p(la), _p(lb), _p(ws), wsb, _p(st),
+                                         _stream(dev))
+    _finish("ssnt_fwd_bwd_debug64", rc, st, check)
+    res = {"loss": loss, "log_alpha": la, "log_beta": lb, "status": st}
+    if grad is not None:
+        res["grad"] = grad
+    if gobs is not None:
+        res["grad_obs"] = gobs
     return res
 
 

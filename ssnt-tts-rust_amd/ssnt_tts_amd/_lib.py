@@ -43,6 +43,9 @@ SIGNATURES = {
                                     c_size_t, P, P]),
     "ssnt_fwd_bwd_sum_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P,
                                         c_size_t, P, P, P, P]),
+    "ssnt_fwd_bwd_debug64_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "ssnt_fwd_bwd_debug64_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P,
+                                            P, P, c_size_t, P, P]),
     "ssnt_fwd_bwd": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "ssnt_v2_fwd_bwd_workspace_size": (c_size_t, [c_int, c_int, c_int, c_bool]),
     "ssnt_v2_fwd_bwd_device": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_bool,

@@ -15,6 +15,22 @@ GOLDEN = ROOT / "tests" / "golden"
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libssnt_tts_c.so)")
     config.addinivalue_line("markers", "slow: long-running case")
+    config.addinivalue_line("markers", "ab: exercises a form only the A/B build reaches (deep rings, "
+                            "selection decode ordering, alternative host waits); deselected unless "
+                            "SSNT_AB_TESTS=1, so a default run counts the product's own paths")
+
+
+def pytest_collection_modifyitems(config, items):
+    # A/B-only forms (include/ssnt_tts_c_ab.h) that no product dispatch reaches: kept runnable
+    # (SSNT_AB_TESTS=1) but out of the default count
+    if os.environ.get("SSNT_AB_TESTS") == "1":
+        return
+    keep, drop = [], []
+    for it in items:
+        (drop if it.get_closest_marker("ab") else keep).append(it)
+    if drop:
+        config.hook.pytest_deselected(items=drop)
+        items[:] = keep
 
 
 @pytest.fixture(scope="session")

@@ -26,7 +26,7 @@ def _eq(gpu_out, ref, keys, ctx=""):
         assert np.array_equal(g, ref[k]), f"{ctx} {k}: gpu={g} ref={ref[k]}"
 
 
-@pytest.fixture(params=[0, 1], ids=["rank", "select"])
+@pytest.fixture(params=[pytest.param(0, id="rank"), pytest.param(1, marks=pytest.mark.ab, id="select")])
 def select_mode(request, gpu):
     """The fused decodes' two step orderings (full rank: the product; selection: forced through
     the A/B build, include/ssnt_tts_c_ab.h) must give identical outputs."""
@@ -38,7 +38,9 @@ def select_mode(request, gpu):
         yield 1
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["sync", "writevalue", "flagkernel"])
+@pytest.fixture(params=[pytest.param(0, marks=pytest.mark.ab, id="sync"),
+                        pytest.param(1, marks=pytest.mark.ab, id="writevalue"),
+                        pytest.param(2, id="flagkernel")])
 def host_sync(request, gpu):
     """The per-step host symbols' three ways of waiting for their kernel (hipStreamSynchronize,
     a hipStreamWriteValue32 completion word, a completion word written by a flag kernel) must

@@ -22,7 +22,7 @@ def _t(x):
     return torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["rank", "select"])
+@pytest.fixture(autouse=True, params=[pytest.param(0, id="rank"), pytest.param(1, marks=pytest.mark.ab, id="select")])
 def select_mode(request, gpu):
     """The fused decodes' two step orderings (full rank: the product; selection: forced through
     the A/B build, include/ssnt_tts_c_ab.h) must give identical outputs."""

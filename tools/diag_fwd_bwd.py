@@ -14,14 +14,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import ssnt_tts_amd as S  # noqa: E402
 
-VARIANT = int(os.environ.get("SSNT_VARIANT", "0"))  # 0 default mix, 2..6 tuning mixes
-NC, NH = {0: (3, 4), 2: (4, 2), 3: (3, 2), 4: (2, 4), 5: (2, 2), 6: (2, 3), 7: (3, 3), 8: (3, 4),
-          13: (3, 4), 14: (3, 4)}[VARIANT]  # 0: the streaming kernel (default), 13 / 14: the rows kernel
+NC, NH = 3, 4  # the streaming kernel's K <= 2 wave mix
 ROLES = ["alpha chain", "beta chain"] + [f"conv {'fb'[i % 2]}{i // 2}" for i in range(2 * NC)] + \
         [f"grad {'fb'[i % 2]}{i // 2}" for i in range(2 * NH)]
 B, T, U = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (256, 200, 80)))
 lib = S.load()
-assert lib.ssnt_fwd_bwd_set_variant(VARIANT) == 0
 lib.ssnt_diag_read.restype = ctypes.c_int
 lib.ssnt_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 dev = torch.device("cuda:0")
@@ -44,7 +41,7 @@ for _ in range(5):
     e1.record()
     torch.cuda.synchronize()
     times.append(e0.elapsed_time(e1) * 1e3)
-print(f"exp={os.environ.get('SSNT_EXP', '0')} launch (incl. wrapper) median {np.median(times):.1f} us")
+print(f"launch (incl. wrapper) median {np.median(times):.1f} us")
 for w, nm in enumerate(ROLES):
     tot, wait, nw, cut, cw = (np.median(d[:, w, i]) for i in range(5))
     c0, c1, c2 = (np.median(d[:, w, i]) for i in (5, 6, 7))

@@ -76,10 +76,13 @@ def _regs(tok: str) -> set[int]:
 
 
 def parse(lines: list[str]):
-    """-> list of (mnemonic, operand tokens, text, function name); labels / directives dropped."""
+    """-> list of (mnemonic, operand tokens, text, function name, address or None); labels /
+    directives dropped. The address is objdump's `// 0000ADDR:` comment (absent in .s files)."""
     insts = []
     fn = "?"
     for raw in lines:
+        am = re.search(r"//\s*([0-9A-Fa-f]{8,}):", raw)
+        addr = int(am.group(1), 16) if am else None
         s = raw.split("//")[0].split(";")[0].rstrip()
         if not s:
             continue
@@ -90,6 +93,7 @@ def parse(lines: list[str]):
         if re.match(r"^[A-Za-z_.$][\w.$]*:", s):  # .s label (function or block)
             if not s.startswith((".L", "$")):
                 fn = s.split(":")[0]
+            insts.append(("<label>", [s.split(":")[0]], s, fn, None))
             continue
         st = s.strip()
         if st.startswith("."):
@@ -99,7 +103,7 @@ def parse(lines: list[str]):
         if not re.match(r"^[a-z][a-z0-9_]*$", mn):
             continue
         ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
-        insts.append((mn, ops, st, fn))
+        insts.append((mn, ops, st, fn, addr))
     return insts
 
 
@@ -112,26 +116,77 @@ def wait_states(mn: str, ops: list[str]) -> int:
     return 1
 
 
-def scan(insts) -> list[str]:
+def _branch_target(insts, j, by_addr, by_label):
+    """Index of the instruction a branch at j jumps to, or None when it cannot be resolved."""
+    mn, ops, _, _, addr = insts[j]
+    if not ops:
+        return None
+    tok = ops[0]
+    if tok in by_label:  # .s input: a label operand
+        return by_label[tok]
+    try:
+        imm = int(tok, 0)
+    except ValueError:
+        return None
+    if addr is None:
+        return None
+    off = imm - 0x10000 if imm >= 0x8000 else imm  # simm16, in dwords, from the next instruction
+    return by_addr.get(addr + 4 + 4 * off)
+
+
+def scan(insts, taken=False) -> list[str]:
+    """Every path from a >64-bit store is followed for NEED wait states. Straight-line code and
+    the fall-through of a conditional branch are always followed (a not-taken
+    s_cbranch does not end the window). A path ends at s_branch, s_setpc or s_endpgm.
+
+    taken=True also follows the target of every branch, counting the branch as one wait state
+    (LLVM's own cross-block count: it pads a loop head after a store + back edge with s_nop 0).
+    While EXEC is unchanged since the store, a taken s_cbranch_execz (or a not-taken
+    s_cbranch_execnz) means the store ran with EXEC = 0 and wrote nothing: no hazard on that
+    path. DESIGN.md 5.1b reports what the taken-branch scan finds and why the product does not
+    assert it."""
+    by_addr = {ins[4]: k for k, ins in enumerate(insts) if ins[4] is not None}
+    by_label = {ins[1][0]: k for k, ins in enumerate(insts) if ins[0] == "<label>"}
     bad = []
-    for i, (mn, ops, text, fn) in enumerate(insts):
+    for i, (mn, ops, text, fn, _) in enumerate(insts):
         if not _WIDE_STORE.match(mn):
             continue
         # data operand: buffer stores "vdata, vaddr, srsrc, soffset"; global/flat "vaddr, vdata, ..."
         data = _regs(ops[0]) if mn.startswith("buffer") else _regs(ops[1] if len(ops) > 1 else "")
         if not data:
             continue
-        ws = 0
-        for j in range(i + 1, min(i + 1 + 4 * NEED, len(insts))):
-            mn2, ops2, text2, _ = insts[j]
-            if ws >= NEED:
-                break
-            if mn2.startswith("v_") and ops2 and _regs(ops2[0]) & data:
-                bad.append(f"{fn}: '{text}' then '{text2}' after {ws} wait state(s)")
-                break
-            if mn2.startswith(("s_branch", "s_cbranch", "s_setpc", "s_endpgm")):
-                break  # (the straight-line successor is checked; branch targets start with waits)
-            ws += wait_states(mn2, ops2)
+        work = [(i + 1, 0, False)]  # (index, wait states so far, EXEC written since the store)
+        seen = set()
+        hit = None
+        while work and hit is None:
+            j, ws, exw = work.pop()
+            while j < len(insts) and ws < NEED and (j, ws, exw) not in seen:
+                seen.add((j, ws, exw))
+                mn2, ops2, text2, _, _ = insts[j]
+                if mn2 == "<label>":
+                    j += 1
+                    continue
+                if mn2.startswith("v_") and ops2 and _regs(ops2[0]) & data:
+                    hit = f"{fn}: '{text}' then '{text2}' after {ws} wait state(s)"
+                    break
+                if mn2.startswith(("s_setpc", "s_endpgm")):
+                    break
+                if mn2.startswith(("s_branch", "s_cbranch")):
+                    if taken:
+                        t = _branch_target(insts, j, by_addr, by_label)
+                        if t is None:
+                            hit = f"{fn}: '{text}' then unresolved branch '{text2}'"
+                            break
+                        if not (mn2 == "s_cbranch_execz" and not exw):
+                            work.append((t, ws + 1, exw))
+                    if mn2.startswith("s_branch") or (mn2 == "s_cbranch_execnz" and not exw):
+                        break
+                if mn2.startswith("s_") and (("saveexec" in mn2) or (ops2 and ops2[0].startswith("exec"))):
+                    exw = True
+                ws += wait_states(mn2, ops2)
+                j += 1
+        if hit:
+            bad.append(hit)
     return bad
 
 
@@ -141,10 +196,14 @@ def main(argv: list[str]) -> int:
         insts = parse(disassemble(Path(a)))
         stores = sum(1 for mn, *_ in insts if _WIDE_STORE.match(mn))
         bad = scan(insts)
+        tk = [x for x in scan(insts, taken=True) if x not in bad]
         total += len(bad)
-        print(f"{a}: {len(insts)} instructions, {stores} wide stores, {len(bad)} hazard(s)")
+        print(f"{a}: {len(insts)} instructions, {stores} wide stores, {len(bad)} hazard(s) on "
+              f"straight-line / fall-through paths, {len(tk)} more through a taken branch")
         for b in bad[:20]:
             print("  ", b)
+        for b in tk[:20]:
+            print("   (taken)", b)
     return 1 if total else 0
 
 
