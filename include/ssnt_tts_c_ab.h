@@ -32,6 +32,8 @@ int ssnt_fwd_bwd_wide_split(int mode);
 int ssnt_fwd_bwd_stream_ring(int r);
 /* fused decodes: -1 default, 0 full rank, 1 selection ordering */
 int ssnt_fused_decode_select(int mode);
+/* tone fused decode: waves its 20-candidate rank is split over (1, 2, 4; -1 the product's choice) */
+int ssnt_fused_decode_tone_waves(int n);
 /* per-step reference symbols: host staging 0 copies / 1 zero-copy; completion 0 stream
  * synchronise / 1 hipStreamWriteValue32 word / 2 flag kernel; both return the previous mode */
 int ssnt_set_host_staging(int mode);

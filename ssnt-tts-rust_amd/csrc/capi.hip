@@ -620,6 +620,8 @@ int ssnt_set_host_sync(int mode) {
 
 // the fused decodes' step ordering: -1 default, 0 full rank, 1 selection
 int ssnt_fused_decode_select(int mode) { return set_fused_decode_select(mode); }
+// waves of the tone fused decode's rank (1, 2, 4; -1 the product's choice)
+int ssnt_fused_decode_tone_waves(int n) { return set_fused_decode_tone_waves(n); }
 
 // the long-row kernel's lane width
 int ssnt_fwd_bwd_wide_lanes(int k) { return set_fwd_bwd_wide_lanes(k); }

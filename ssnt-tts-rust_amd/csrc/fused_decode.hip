@@ -35,10 +35,8 @@ namespace {
 using namespace dec;
 
 constexpr int kAhead = 8;    // input rows in flight
-// the rank counts by sign bits from this many compares per lane up (tuning knob: -D override)
-#ifndef SSNT_DEC_SIGN_MIN
-#define SSNT_DEC_SIGN_MIN 16
-#endif
+// the rank counts by sign bits from this many compares per lane up
+constexpr int kSignMin = 16;
 
 // Diagnostic build only (-DSSNT_DIAG, `make lib-diag`): s_memtime cycle totals of the register
 // kernel's step phases for utterance 0 (tools/diag_decode.py): 0 candidate generation, 1 rank /
@@ -113,8 +111,11 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 // (each compares every candidate with 16 of the keys; the partial counts cross through LDS, one
 // barrier per step), everything else runs identically in each wave, and wave 0 alone writes
 // outputs. The 64 compares of one wave were a third of the step.
-constexpr int fused_waves(Variant v, int nmax, bool sel) {
-  return (nmax == 64 && v != Variant::V1 && !sel) ? 4 : 1;
+// Tone's 20 candidates (NMAX 32: two in-wave replicas) can split their rank over TW waves the
+// same way (each wave counts JN / TW of its replica's keys): TW is a template parameter, chosen by
+// the launcher (kToneWaves; the A/B build's ssnt_fused_decode_tone_waves overrides it).
+constexpr int fused_waves(Variant v, int nmax, bool sel, int tw = 1) {
+  return (nmax == 64 && v != Variant::V1 && !sel) ? 4 : (nmax == 32 && v == Variant::Tone && !sel) ? tw : 1;
 }
 
 struct RegLayout {
@@ -143,12 +144,12 @@ struct RegLayout {
 // compiler is told one wave per SIMD, so it may spend registers on keeping loads in flight (its
 // default occupancy target of 8 waves caps a wave at 64 VGPRs, which serialised the rank's
 // broadcast key reads into one LDS round trip per two keys).
-template <Variant V, bool STAGED, int NMAX, bool WHOLE, bool SEL>
-__global__ __launch_bounds__(64 * fused_waves(V, NMAX, SEL)) __attribute__((amdgpu_waves_per_eu(1, 1)))
+template <Variant V, bool STAGED, int NMAX, bool WHOLE, bool SEL, int TW = 1>
+__global__ __launch_bounds__(64 * fused_waves(V, NMAX, SEL, TW)) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool kV1 = V == Variant::V1, kV2 = V == Variant::V2;
-  constexpr int kNW = fused_waves(V, NMAX, SEL);
+  constexpr int kNW = fused_waves(V, NMAX, SEL, TW);
   // sort and compaction through LDS records (v2 / tone beyond 16 candidates, staged v1); the
   // other forms permute the fields across lanes
   constexpr bool kRecs = (NMAX > 16 && !kV1) || (kV1 && STAGED);
@@ -473,7 +474,7 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
     // kSign (>= 32 compares per lane): a 63-bit key (high word shifted by 31), so a difference of
     // two keys never overflows and its sign bit is the comparison; else (khi, 63 - c) as a pair
     constexpr int kJN = kRep8 ? 1 : NMAX / kReps;
-    constexpr bool kSign = kJN >= SSNT_DEC_SIGN_MIN;
+    constexpr bool kSign = kJN >= kSignMin;
     const u64 key = ((u64)(valid ? khi : 0u) << (kSign ? 31 : 32)) | (unsigned)(63 - c);
     int rank = 0;
     int rank16 = -1;  // 16 * rank when the partial counts arrive premultiplied (four waves)
@@ -513,6 +514,28 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       }
       return r;
     };
+    // several waves: each wave's partial counts meet in LDS (double-buffered by step parity: a
+    // wave a step ahead writes the other buffer) across one barrier that orders LDS only (no
+    // wait for the row prefetch's global loads); the sum comes back premultiplied by 16
+    auto wave_sum16 = [&](int part) {
+      int* xr = xrank + (s & 1) * 64 * kNW;
+      xr[lane * kNW + wv] = part << 4;  // (premultiplied: the sum is a record's byte offset)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      int r16;
+      if constexpr (kNW == 4) {
+        const int4 pr = *reinterpret_cast<const int4*>(xr + lane * kNW);
+        r16 = (pr.x + pr.y) + (pr.z + pr.w);
+      } else if constexpr (kNW == 2) {
+        const int2 pr = *reinterpret_cast<const int2*>(xr + lane * kNW);
+        r16 = pr.x + pr.y;
+      } else {
+        r16 = part << 4;  // (one wave: never called)
+      }
+      lds_order();
+      return r16;
+    };
     if constexpr (kRep8) {
       // lane 8x + y compares its candidate y with candidate x (read from lane x): bit 8x + y of
       // the ballot says y sorts before x, so candidate x's rank is the popcount of byte x
@@ -525,10 +548,13 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       // replica r counts the keys [r JN, (r + 1) JN) of replica 0 that beat its candidate (reads
       // broadcast within the replica); the partial counts are summed across replicas by swapping
       // 16-lane rows and 32-lane halves
+      // (several waves: each wave counts JN / kNW of those keys, and the waves' partial counts
+      // are summed like the four-wave rank below)
       constexpr int JN = NMAX / kReps;
+      constexpr int JW = JN / kNW;
       keys[lane] = kSign ? 0ull - key : key;
       lds_order();
-      rank = count_beats(keys + (lane / NMAX) * JN, std::integral_constant<int, JN>{});
+      rank = count_beats(keys + (lane / NMAX) * JN + JW * wv, std::integral_constant<int, JW>{});
       lds_order();
       if constexpr (kReps == 4) {
         const auto r16 = __builtin_amdgcn_permlane16_swap(rank, rank, false, false);
@@ -536,6 +562,10 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       }
       const auto r32 = __builtin_amdgcn_permlane32_swap(rank, rank, false, false);
       rank = (int)(r32[0] + r32[1]);
+      if constexpr (kNW > 1) {
+        rank = wave_sum16(rank) >> 4;
+        rank16 = (gbase | rank) << 4;
+      }
     } else if constexpr (kNW > 1) {
       // wave wv counts the keys [16 wv, 16 wv + 16) of its own copy; the partial counts meet in
       // LDS (double-buffered by step parity: a wave a step ahead writes the other buffer) across
@@ -543,16 +573,8 @@ void k_fused_reg(FusedDecodeArgs a, int hist_lds) {
       keys[lane] = kSign ? 0ull - key : key;
       lds_order();
       const int part = count_beats(keys + (64 / kNW) * wv, std::integral_constant<int, 64 / kNW>{});
-      int* xr = xrank + (s & 1) * 64 * kNW;
-      xr[lane * kNW + wv] = part << 4;  // (premultiplied: the sum is the record's byte offset)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      static_assert(kNW == 4, "one 16-byte read of the partial counts");
-      const int4 pr = *reinterpret_cast<const int4*>(xr + lane * kNW);
-      rank16 = (pr.x + pr.y) + (pr.z + pr.w);
+      rank16 = wave_sum16(part);
       rank = rank16 >> 4;
-      lds_order();
     } else {
       keys[lane] = kSign ? 0ull - key : key;
       lds_order();
@@ -899,12 +921,20 @@ constexpr size_t kMaxLds = 150 * 1024;
 // ordering of the register kernel's step: the full rank. The selection ordering (SEL) is
 // bit-identical and measured slower at every BASELINE shape; it is compiled
 // only into the A/B build (-DSSNT_AB: ssnt_fused_decode_select 0 full rank, 1 selection).
+// waves of tone's replicated rank (1, 2 or 4); the A/B build can override it per process
+constexpr int kToneWaves = 1;
 #ifdef SSNT_AB
 std::atomic<int> g_select{-1};
 bool use_select() { return g_select.load(std::memory_order_relaxed) == 1; }
+std::atomic<int> g_tone_waves{-1};
+int tone_waves() {
+  const int t = g_tone_waves.load(std::memory_order_relaxed);
+  return t > 0 ? t : kToneWaves;
+}
 #define SSNT_SEL_OR_RANK(sel, RANK, SELK) ((sel) ? (SELK) : (RANK))
 #else
 constexpr bool use_select() { return false; }
+constexpr int tone_waves() { return kToneWaves; }
 #define SSNT_SEL_OR_RANK(sel, RANK, SELK) (RANK)
 #endif
 
@@ -929,7 +959,8 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
     const bool staged = V != Variant::V1 || 2 * (size_t)a.U <= 64 * (size_t)kV1Regs;
     const bool sel = use_select();
     const int nmax = n <= 8 ? 8 : n <= 16 ? 16 : n <= 32 ? 32 : 64;
-    const int nw = staged ? fused_waves(V, nmax, sel) : 1;
+    const int tw = V == Variant::Tone ? tone_waves() : 1;
+    const int nw = staged ? fused_waves(V, nmax, sel, tw) : 1;
     const bool whole = RegLayout(V, a.W, a.T, a.U, true, staged, true, nw).total <= kMaxLds;
     const bool hist_lds = whole || RegLayout(V, a.W, a.T, a.U, true, staged, false, nw).total <= kMaxLds;
     const size_t lds = RegLayout(V, a.W, a.T, a.U, hist_lds, staged, whole, nw).total;
@@ -944,6 +975,12 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
                                   launch_with_lds(k_fused_reg<V, false, 64, WH, true>, lds, a.B, st, a, h));
         }
         return (int)SSNT_ERR_UNSUPPORTED;
+      }
+      if constexpr (V == Variant::Tone && NM == 32) {
+        if (!sel && tw == 2)
+          return launch_with_lds(k_fused_reg<V, true, NM, WH, false, 2>, lds, a.B, st, a, h, 2);
+        if (!sel && tw == 4)
+          return launch_with_lds(k_fused_reg<V, true, NM, WH, false, 4>, lds, a.B, st, a, h, 4);
       }
       return SSNT_SEL_OR_RANK(sel, launch_with_lds(k_fused_reg<V, true, NM, WH, false>, lds, a.B, st, a, h,
                                                    fused_waves(V, NM, false)),
@@ -992,6 +1029,11 @@ int diag_decode_read(void* host, size_t bytes) {
 int set_fused_decode_select(int mode) {
   if (mode < -1 || mode > 1) return SSNT_ERR_INVALID_ARG;
   g_select.store(mode);
+  return SSNT_OK;
+}
+int set_fused_decode_tone_waves(int n) {
+  if (n != -1 && n != 1 && n != 2 && n != 4) return SSNT_ERR_INVALID_ARG;
+  g_tone_waves.store(n);
   return SSNT_OK;
 }
 #endif

@@ -58,7 +58,10 @@ constexpr int kChainPrefetch(int R) { return R >= 16 ? 4 : 2; }  // factor rows 
 template <int K>
 constexpr int conv_depth() { return K <= 2 ? 8 : (K <= 4 ? 4 : 2); }  // converter prefetch rows
 
-template <int K, bool OBS, bool LDS, int kNC, int kNH, int kRingSel, bool NV>
+// DBG: debug rows requested (log_alpha / log_beta, f32 logs or the raw split-exponent state of
+// ssnt_fwd_bwd_debug64_device) -- a separate instance, so the product's carries neither the
+// debug path nor its pointers (their SGPRs spilled into VGPR lanes in the hot loops)
+template <int K, bool OBS, bool LDS, int kNC, int kNH, int kRingSel, bool NV, bool DBG>
 __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream(FwdBwdArgs a) {
   constexpr int kWaves = 2 + 2 * kNC + 2 * kNH;
   // kRingSel: ring slots (0 = default; 16 / 32: the A/B build's deep rings)
@@ -83,10 +86,10 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
   const float* lo = OBS ? a.log_obs + (size_t)b * TU : nullptr;
   float* g = a.grad ? a.grad + (size_t)b * TU * 2 : nullptr;
   float* go = (OBS && a.grad_obs) ? a.grad_obs + (size_t)b * TU : nullptr;
-  float* la = a.log_alpha ? a.log_alpha + (size_t)b * TU : nullptr;
-  float* lb = a.log_beta ? a.log_beta + (size_t)b * TU : nullptr;
-  int* lae = (la && a.log_alpha_e) ? a.log_alpha_e + (size_t)b * TU : nullptr;  // raw-state debug
-  int* lbe = (lb && a.log_beta_e) ? a.log_beta_e + (size_t)b * TU : nullptr;
+  float* la = (DBG && a.log_alpha) ? a.log_alpha + (size_t)b * TU : nullptr;
+  float* lb = (DBG && a.log_beta) ? a.log_beta + (size_t)b * TU : nullptr;
+  int* lae = (DBG && la && a.log_alpha_e) ? a.log_alpha_e + (size_t)b * TU : nullptr;  // raw-state debug
+  int* lbe = (DBG && lb && a.log_beta_e) ? a.log_beta_e + (size_t)b * TU : nullptr;
   const int p0 = K * lane;
   const bool act = p0 < U;
   const int pr = act ? p0 : Up - K;  // LDS read position (clamped for lanes past U)
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
 #pragma unroll
     for (int j = 0; j < 2 * K; ++j) z[j] = 0.0f;
 #pragma unroll
-    for (int j = 0; j < K; ++j) ninf[j] = a.log_alpha_e ? 0.0f : -__builtin_inff();  // raw: mantissa 0
+    for (int j = 0; j < K; ++j) ninf[j] = (DBG && a.log_alpha_e) ? 0.0f : -__builtin_inff();  // raw: mantissa 0
     for (int s = from + w0; s < T; s += wstep) {
       if (g) SSNT_GST2(z, g, s);
       if (go) SSNT_GST1(z, go, s);
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
       if (lane == 0) {
         ctl->z = z;
         publish_loss(a, b, (z.m == 0.0f) ? inf_loss : 0.0f - xf_log(z), tag);
-        if (a.z_state) {
+        if (DBG && a.z_state) {
           a.z_state[2 * b] = z.m;
           a.z_state[2 * b + 1] = __builtin_bit_cast(float, z.e);
         }
@@ -355,7 +358,7 @@ __global__ __launch_bounds__(64 * (2 + 2 * kNC + 2 * kNH)) void k_fwd_bwd_stream
           if constexpr (OBS) {
             if (go) gst<K, 1, NV>(gob, brsrc(go + (size_t)s * U, U * 4u), p0);
           }
-          if (la || lb) {  // debug outputs (slow path)
+          if (DBG && (la || lb)) {  // debug outputs (the DBG instance only)
             float va[K], vb[K], ea[K], eb[K];
 #pragma unroll
             for (int q = 0; q < K; ++q) {
@@ -736,9 +739,11 @@ inline bool aligned_to(const void* p, uintptr_t m) { return (reinterpret_cast<ui
 
 template <int K, bool OBS, bool LDS, int NC, int NH, int RS, bool NV>
 int launch_stream_kernel(const FwdBwdArgs& a, size_t lds, hipStream_t st) {
-  auto kern = k_fwd_bwd_stream<K, OBS, LDS, NC, NH, RS, NV>;
-  note_fwd_bwd_dispatch("k_fwd_bwd_stream<K=%d,OBS=%d,LDS=%d,NC=%d,NH=%d,RS=%d,NV=%d>", K, (int)OBS,
-                        (int)LDS, NC, NH, RS, (int)NV);
+  const bool dbg = a.log_alpha || a.log_beta;
+  auto kern = dbg ? k_fwd_bwd_stream<K, OBS, LDS, NC, NH, RS, NV, true>
+                  : k_fwd_bwd_stream<K, OBS, LDS, NC, NH, RS, NV, false>;
+  note_fwd_bwd_dispatch("k_fwd_bwd_stream<K=%d,OBS=%d,LDS=%d,NC=%d,NH=%d,RS=%d,NV=%d%s>", K, (int)OBS,
+                        (int)LDS, NC, NH, RS, (int)NV, dbg ? ",DBG" : "");
   // dynamic LDS above 64 KiB needs the attribute; it is per device, so it is set on every such
   // launch (a host-side call, no device work) rather than cached in a process-wide flag
   if (lds > 64 * 1024)

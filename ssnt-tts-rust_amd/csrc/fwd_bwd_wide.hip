@@ -53,16 +53,9 @@ namespace {
 // the kernel near 3 TB/s); K = 2 has twice the bytes per row and the registers for 8.
 // SPLIT phase 1 at K = 1 keeps 32 rows in flight (at most 2 waves per SIMD leave it the
 // registers; configs[4]: 660 -> 625 us), one workgroup per direction 16 (32 measured slower there).
-// (build-time overrides for tuning studies: SSNT_W_D1 / SSNT_W_D2, phase 1 / 2 at K = 1)
-#ifndef SSNT_W_D1
-#define SSNT_W_D1 16
-#endif
-#ifndef SSNT_W_D2
-#define SSNT_W_D2 16
-#endif
 template <int K, int PHASE, bool SPLIT>
 constexpr int block_steps() {
-  return K == 1 ? (PHASE == 1 ? (SPLIT ? 32 : SSNT_W_D1) : SSNT_W_D2) : 8;
+  return K == 1 ? (PHASE == 1 ? (SPLIT ? 32 : 16) : 16) : 8;
 }
 constexpr int kRB = 64;        // hand-off ring slots (steps) per wave
 constexpr int kMaxNW = 8;      // waves per direction: U <= 512 (K = 1) / 1024 (K = 2)

@@ -67,6 +67,7 @@ int stream_ring();
 int set_fwd_bwd_wide_lanes(int k);  // positions per lane of the long-row kernel (1 or 2)
 int set_fwd_bwd_wide_split(int mode);  // two workgroups per direction (-1 auto, 0 off, 1 on)
 int set_fused_decode_select(int mode);  // -1 default, 0 full rank, 1 selection
+int set_fused_decode_tone_waves(int n);  // -1 default, 1 / 2 / 4 waves for tone's rank
 #else
 constexpr int stream_ring() { return 0; }
 #endif

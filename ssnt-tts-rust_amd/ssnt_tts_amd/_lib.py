@@ -78,6 +78,7 @@ AB_SIGNATURES = {
     "ssnt_fwd_bwd_wide_split": (c_int, [c_int]),
     "ssnt_fwd_bwd_stream_ring": (c_int, [c_int]),
     "ssnt_fused_decode_select": (c_int, [c_int]),
+    "ssnt_fused_decode_tone_waves": (c_int, [c_int]),
     "ssnt_set_host_staging": (c_int, [c_int]),
     "ssnt_set_host_sync": (c_int, [c_int]),
     "ssnt_diag_step_clock": (c_int, [c_int, c_void_p]),
@@ -151,6 +152,7 @@ class use_ab:
             ab.ssnt_fwd_bwd_wide_split(-1)
             ab.ssnt_fwd_bwd_stream_ring(0)
             ab.ssnt_fused_decode_select(-1)
+            ab.ssnt_fused_decode_tone_waves(-1)
             ab.ssnt_set_host_staging(1)
             ab.ssnt_set_host_sync(2)
             _active = None

@@ -125,6 +125,22 @@ def test_v2_fused_random(gpu, oracle, seed):
         c["zero_duration_id"], c["allow_skip"], c["test_mode"], f"seed={seed}")
 
 
+PRODUCT_TONE_WAVES = 1  # fused_decode.hip kToneWaves
+
+
+@pytest.fixture(params=[pytest.param(w, id=f"tone{w}w", marks=() if w == PRODUCT_TONE_WAVES else pytest.mark.ab)
+                        for w in (1, 2, 4)])
+def tone_waves(request, gpu):
+    """Tone's 20-candidate rank split over 1, 2 or 4 waves (the product's choice, and the others
+    forced through the A/B build): identical outputs."""
+    if request.param == PRODUCT_TONE_WAVES:
+        yield request.param
+        return
+    with gpu.use_ab() as ab:
+        assert ab.ssnt_fused_decode_tone_waves(request.param) == 0
+        yield request.param
+
+
 def _tone(gpu, oracle, lg, il, eid, ctx):
     o = oracle.tone_lattice_decode(lg, il, eid)
     g = gpu.tone_latent_lattice_beam_search_decode(_t(lg), _t(il), lg.shape[2], eid)
@@ -132,7 +148,7 @@ def _tone(gpu, oracle, lg, il, eid, ctx):
 
 
 @pytest.mark.parametrize("tie_rich", [False, True])
-def test_tone_config5(gpu, oracle, tie_rich):
+def test_tone_config5(gpu, oracle, tone_waves, tie_rich):
     """B=64 T=I=400 C=5 W=4 (20 candidates), ragged input lengths up to the step count."""
     B, T, W, C = 64, 400, 4, 5
     lg = oracle.synth_tone_logits(B, T, W, C, seed=20 + tie_rich, tie_rich=tie_rich)
@@ -148,7 +164,7 @@ def test_tone_more_candidates_than_lanes(gpu, oracle):
 
 
 @pytest.mark.parametrize("seed", range(150))
-def test_tone_fused_random(gpu, oracle, seed):
+def test_tone_fused_random(gpu, oracle, tone_waves, seed):
     c = dc.fused_tone_case(seed)
     _tone(gpu, oracle, c["logits"], c["input_length"], c["empty_tone_id"], f"seed={seed}")
 
@@ -287,7 +303,7 @@ def test_v2_history_beyond_lds(gpu, oracle):
     (3000, 4, 5, "chunked flush, history in LDS"),
     (500, 64, 1, "history beyond LDS: k_fused_paths"),
 ])
-def test_tone_long_history_layouts(gpu, oracle, T, W, C, ctx):
+def test_tone_long_history_layouts(gpu, oracle, tone_waves, T, W, C, ctx):
     B = 4
     lg = oracle.synth_tone_logits(B, T, W, C, seed=T + C, tie_rich=True)
     il = np.random.default_rng(T).integers(T // 2, T + 1, size=B).astype(np.int32)
