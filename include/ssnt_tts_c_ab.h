@@ -25,7 +25,8 @@ extern "C" {
 /* forward-backward kernel: 0 default dispatch, 1 two-wave kernel, 2 segmented kernel at every U
  * it takes; env SSNT_FWD_BWD_KERNEL=simple selects 1 at first use */
 int ssnt_fwd_bwd_set_variant(int variant);
-/* segmented kernel: positions per lane (1 or 2) and the workgroup split (-1 auto, 0, 1) */
+/* segmented kernel: positions per lane (1 or 2) and the workgroup split (-1 auto, 0, 1; 2: phase 2
+ * only, a study form) */
 int ssnt_fwd_bwd_wide_lanes(int k);
 int ssnt_fwd_bwd_wide_split(int mode);
 /* streaming kernel: 0 default rings; 16 / 32 converter ring slots with the rows in the workspace */

@@ -809,7 +809,7 @@ inline WideLayout wide_layout(int B, int T, int U) {
 // -1 auto (default): split when the unsplit grid would leave most CUs idle (8B <= CUs) or for
 // the heaviest workgroups (K = 2, 8 waves) when 4B <= CUs -- measured per shape, DESIGN.md 5.2
 // (configs[4], B=64 U=400: one workgroup 604 vs split 637 us; B=32: 565 vs 511; B=64 U=1024:
-// 868 vs 749); 0 never; 1 whenever NW >= 2
+// 868 vs 749); 0 never; 1 whenever NW >= 2; 2 (A/B study) phase 2 only
 #ifdef SSNT_AB
 std::atomic<int> g_wide_split{-1};  // A/B build: ssnt_fwd_bwd_wide_split
 int wide_split_mode() { return g_wide_split.load(std::memory_order_relaxed); }
@@ -848,6 +848,14 @@ int launch_wide(const FwdBwdArgs& a, hipStream_t st) {
   } else if (NW >= 2 && mode == -1) {
     const int cus = device_cus();
     split = 8 * a.B <= cus || (K == 2 && NW == kMaxNW && 4 * a.B <= cus);
+  }
+  if (NW >= 2 && mode == 2) {  // A/B study: phase 1 in one workgroup per direction, phase 2 split
+    if (hipMemsetAsync(gd.ctr, 0, l.ctr, st) != hipSuccess) return SSNT_ERR_HIP;
+    note_fwd_bwd_dispatch("k_fwd_bwd_wide<K=%d,OBS=%d,DBG=%d,NW=%d>+SPLIT2", K, (int)OBS, (int)DBG, NW);
+    hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 1, DBG, false>), dim3(a.B, 2), dim3(64 * NW), 0, st, a, gd);
+    if (hipGetLastError() != hipSuccess) return SSNT_ERR_HIP;
+    hipLaunchKernelGGL((k_fwd_bwd_wide<K, OBS, 2, DBG, true>), dim3(4 * a.B), dim3(64 * (gd.NWp + 1)), 0, st, a, gd);
+    return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
   }
   if (split) {
     if (hipMemsetAsync(gd.ctr, 0, l.ctr, st) != hipSuccess) return SSNT_ERR_HIP;
@@ -911,7 +919,7 @@ int set_fwd_bwd_wide_lanes(int k) {
 }
 
 int set_fwd_bwd_wide_split(int mode) {
-  if (mode < -1 || mode > 1) return SSNT_ERR_INVALID_ARG;
+  if (mode < -1 || mode > 2) return SSNT_ERR_INVALID_ARG;
   g_wide_split.store(mode);
   return SSNT_OK;
 }

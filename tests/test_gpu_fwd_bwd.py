@@ -218,7 +218,9 @@ def test_config5_long_form_bit_exact(gpu, oracle):
     _assert_bit_exact(g, o, ["loss", "grad"])
 
 
-@pytest.fixture(params=[(1, 1), (1, 0), (2, 1), (2, 0)], ids=["K1", "K1-one-wg", "K2", "K2-one-wg"])
+@pytest.fixture(params=[pytest.param((1, 1), id="K1"), pytest.param((1, 0), id="K1-one-wg"),
+                        pytest.param((2, 1), id="K2"), pytest.param((2, 0), id="K2-one-wg"),
+                        pytest.param((1, 2), id="K1-split2", marks=pytest.mark.ab)])
 def wide_lanes(request, gpu):
     """The long-row kernel's two lane widths (positions per lane), each with a direction's
     segments split over two workgroups (global hand-off) and in one workgroup, must be

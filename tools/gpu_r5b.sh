@@ -14,3 +14,6 @@ timeout -k 10 300 python3 tools/ab_tone_waves.py > gpurun_out/${TAG}_tone_waves.
 cat gpurun_out/${TAG}_tone_waves.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_dec -o kt -- python3 tools/prof_decode.py 10 > gpurun_out/${TAG}_dec.log 2>&1 || exit 1
 cut -d, -f1-4 gpurun_out/${TAG}_dec/kt_kernel_stats.csv | head -12
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_long -o kt -- python3 tools/ab_long_modes.py 0 1 2 > gpurun_out/${TAG}_long.log 2>&1 || exit 1
+grep -h split_mode gpurun_out/${TAG}_long.log
+cut -d, -f1-4 gpurun_out/${TAG}_long/kt_kernel_stats.csv | grep wide
