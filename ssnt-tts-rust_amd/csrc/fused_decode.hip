@@ -921,7 +921,9 @@ constexpr size_t kMaxLds = 150 * 1024;
 // ordering of the register kernel's step: the full rank. The selection ordering (SEL) is
 // bit-identical and measured slower at every BASELINE shape; it is compiled
 // only into the A/B build (-DSSNT_AB: ssnt_fused_decode_select 0 full rank, 1 selection).
-// waves of tone's replicated rank (1, 2 or 4); the A/B build can override it per process
+// waves of tone's replicated rank (1, 2 or 4); the A/B build can override it per process. One:
+// at configs[4] two waves measured 202 us and four 215 us against 189 us for one
+// (profiles/r5b_tone_waves.json) -- the step's LDS round trips, not its 16 compares, set it
 constexpr int kToneWaves = 1;
 #ifdef SSNT_AB
 std::atomic<int> g_select{-1};
@@ -976,12 +978,14 @@ int launch_variant(const FusedDecodeArgs& a, hipStream_t st) {
         }
         return (int)SSNT_ERR_UNSUPPORTED;
       }
-      if constexpr (V == Variant::Tone && NM == 32) {
+#ifdef SSNT_AB
+      if constexpr (V == Variant::Tone && NM == 32) {  // (A/B study forms; measured slower)
         if (!sel && tw == 2)
           return launch_with_lds(k_fused_reg<V, true, NM, WH, false, 2>, lds, a.B, st, a, h, 2);
         if (!sel && tw == 4)
           return launch_with_lds(k_fused_reg<V, true, NM, WH, false, 4>, lds, a.B, st, a, h, 4);
       }
+#endif
       return SSNT_SEL_OR_RANK(sel, launch_with_lds(k_fused_reg<V, true, NM, WH, false>, lds, a.B, st, a, h,
                                                    fused_waves(V, NM, false)),
                               launch_with_lds(k_fused_reg<V, true, NM, WH, true>, lds, a.B, st, a, h,

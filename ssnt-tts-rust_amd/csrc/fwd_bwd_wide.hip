@@ -679,12 +679,23 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
     WRows<K> wr[kDepth];
     if (dir == 0) {
       // ---------------- alpha: rows M..S-1, gradient rows s >= M ----------------
+      // (K = 1: beta[s+1] at p0 and p0+1 in ONE 16-byte load -- a vector-memory instruction
+      // fewer per step; the step holds ~4 in flight per row and vmcnt counts at most 63)
+      const bool nb_ok = p0 + K < U;
       auto load_rows = [&](int s, WRows<K>& r) __attribute__((always_inline)) {  // beta[s+1] (+ position p0+K), beta[s]
         const int sn = uni(min(s + 1, S - 1));
-        ld_row(sn, r.r0);
-        const f32x2 x = rbuf_ld2(rows_r, vnb8, so8(sn), 0);
-        r.nb[0] = x.x;
-        r.nb[1] = x.y;
+        if constexpr (K == 1) {
+          const f32x4 x = rbuf_ld4(rows_r, vo8[0], so8(sn), 0);
+          r.r0[0] = x.x;
+          r.r0[1] = x.y;
+          r.nb[0] = nb_ok ? x.z : 0.0f;  // (past U: what the out-of-range load returned)
+          r.nb[1] = nb_ok ? x.w : 0.0f;
+        } else {
+          ld_row(sn, r.r0);
+          const f32x2 x = rbuf_ld2(rows_r, vnb8, so8(sn), 0);
+          r.nb[0] = x.x;
+          r.nb[1] = x.y;
+        }
         if constexpr (OBS) {
           ld_row(s == M ? T : min(s, S - 1), r.r1);
           r.nob = rbuf_ld1(lo_r, vnb4, so4(min(s + 1, T - 1)), 0);

@@ -462,25 +462,20 @@ __global__ __launch_bounds__(kF4Threads) void k_f4_sweep(V2FwdBwdArgs a) {
 template <int DC>
 constexpr int f4_grad_threads() { return DC <= 16 ? 64 : DC <= 32 ? 128 : 256; }
 
-// steps per gradient workgroup: the per-utterance setup (durations, lengths, Z) is paid once
-// per kF4GradSteps steps, and the rows of step t + 1 load into registers while step t sums
-constexpr int kF4GradSteps = 8;
-// window cells per thread held in registers for that prefetch (wider windows load per step)
-constexpr int kF4GradPf = 8;
-
-// gradients of steps t = blockIdx.y * kF4GradSteps + (0 .. kF4GradSteps-1) (and the debug beta
-// rows t); rows t >= I: zeros / -inf
+// gradients of step t = blockIdx.y (and the debug beta row t); rows t >= I: zeros / -inf
 template <int DC>
 __global__ __launch_bounds__(f4_grad_threads<DC>()) void k_f4_grad(V2FwdBwdArgs a) {
   constexpr int kF4GradThreads = f4_grad_threads<DC>();
   constexpr int kF4GradWaves = kF4GradThreads / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int b = blockIdx.x, t0 = blockIdx.y * kF4GradSteps;
+  const int b = blockIdx.x, t = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int D = a.D, X = a.X, Imax = a.Imax, Wc = a.Wcap;
   int* dur = reinterpret_cast<int*>(smem);
   xf* at = reinterpret_cast<xf*>(smem + ((D * 4 + 15) & ~15));  // alpha row t (+ zero cell Wc)
   xf* bn = at + Wc + 1;                                             // beta row t+1
+  float* g = a.grad ? a.grad + ((size_t)b * Imax + (t < Imax ? t : 0)) * D : nullptr;
+  float* lb = a.log_beta ? a.log_beta + ((size_t)b * (Imax + 1) + t) * X : nullptr;
   const F4Ws W = f4_ws(a);
   for (int i = tid; i < D; i += kF4GradThreads) dur[i] = a.table[i];
   lds_sync();
@@ -488,113 +483,57 @@ __global__ __launch_bounds__(f4_grad_threads<DC>()) void k_f4_grad(V2FwdBwdArgs 
   const bool ok = f4_setup(a, b, dur, u, false);
   const xf Z = ok ? W.z[b] : xf_zero();
   const bool live = ok && Z.m != 0.0f;
+  if (lb) {
+    int lo = 0, hi = -1;
+    if (live && t <= u.I) f4_window(u, t, lo, hi);
+    const xf* br = W.beta + ((size_t)b * (Imax + 1) + t) * Wc;
+    for (int x = tid; x < X; x += kF4GradThreads)
+      lb[x] = (x >= lo && x <= hi) ? xf_log(br[x - lo]) : -__builtin_inff();
+  }
+  if (t >= Imax || !g) return;
+  if (!live || t >= u.I) {
+    for (int i = tid; i < D; i += kF4GradThreads) g[i] = 0.0f;
+    return;
+  }
+  int lo, hi, nlo, nhi;
+  f4_window(u, t, lo, hi);
+  f4_window(u, t + 1, nlo, nhi);
+  const xf* ga = W.alpha + ((size_t)b * (Imax + 1) + t) * Wc;
+  const xf* gb = W.beta + ((size_t)b * (Imax + 1) + t + 1) * Wc;
+  for (int k = tid; k <= hi - lo; k += kF4GradThreads) at[k] = ga[k];
+  if (tid == 0) at[Wc] = xf_zero();
+  for (int k = tid; k <= nhi - nlo; k += kF4GradThreads) bn[k] = gb[k];
+  lds_sync();
   const float izm = 1.0f / Z.m;
   const int ize = -Z.e;
+  const unsigned span = hi >= lo ? (unsigned)(hi - lo) : 0u;
+  if (hi < lo) lo = 1 << 29;  // empty alpha window: every offset out of range
   constexpr int NCW = (DC + kF4GradWaves - 1) / kF4GradWaves;  // classes per wave
+  xf acc[NCW];
   int di[NCW];
 #pragma unroll
   for (int j = 0; j < NCW; ++j) {
+    acc[j] = xf_zero();
     const int i = wave + j * kF4GradWaves;
     di[j] = i < D ? dur[i] : 0;
   }
-  const int t1 = min(t0 + kF4GradSteps, Imax + 1);  // steps of this workgroup: [t0, t1)
-  // debug beta rows (their own pass: the sums below never read them from global memory)
-  if (a.log_beta) {
-    for (int t = t0; t < t1; ++t) {
-      float* lb = a.log_beta + ((size_t)b * (Imax + 1) + t) * X;
-      int lo = 0, hi = -1;
-      if (live && t <= u.I) f4_window(u, t, lo, hi);
-      const xf* br = W.beta + ((size_t)b * (Imax + 1) + t) * Wc;
-      for (int x = tid; x < X; x += kF4GradThreads)
-        lb[x] = (x >= lo && x <= hi) ? xf_log(br[x - lo]) : -__builtin_inff();
+  for (int x = nlo + ((lane - nlo) & 63); x <= nhi; x += 64) {
+    const xf bv = bn[x - nlo];
+#pragma unroll
+    for (int j = 0; j < NCW; ++j) {
+      // a term outside the window is an exact zero: adding it leaves a normalized (or zero)
+      // partial unchanged, so the select is the oracle's skip
+      const unsigned yr = (unsigned)(x - di[j] - lo);
+      const xf av = at[yr <= span ? (int)yr : Wc];  // (zero cell: the oracle's skip)
+      acc[j] = xf_add(acc[j].m, acc[j].e, av.m * bv.m, av.e + bv.e);
     }
   }
-  if (!a.grad) return;
-  // steps that have a gradient row: [t0, tg); of those, [t0, tl) are live (t < I)
-  const int tg = min(t1, Imax);
-  const int tl = live ? min(tg, u.I) : t0;
-  for (int t = max(tl, t0); t < tg; ++t) {
-    float* g = a.grad + ((size_t)b * Imax + t) * D;
-    for (int i = tid; i < D; i += kF4GradThreads) g[i] = 0.0f;
-  }
-  if (tl <= t0) return;
-  // rows of step t: alpha row t over its window [lo, hi], beta row t+1 over [nlo, nhi]
-  struct Rows {
-    int lo, hi, nlo, nhi;
-    xf pa[kF4GradPf], pb[kF4GradPf];
-    float lgt;  // the class log-prob this thread stores (thread < D)
-  };
-  const bool regs = Wc <= kF4GradThreads * kF4GradPf;  // (uniform) windows fit the prefetch
-  auto fetch = [&](int t, Rows& r) {
-    f4_window(u, t, r.lo, r.hi);
-    f4_window(u, t + 1, r.nlo, r.nhi);
-    const xf* ga = W.alpha + ((size_t)b * (Imax + 1) + t) * Wc;
-    const xf* gb = W.beta + ((size_t)b * (Imax + 1) + t + 1) * Wc;
-    if (regs) {
-#pragma unroll
-      for (int j = 0; j < kF4GradPf; ++j) {
-        const int k = tid + kF4GradThreads * j;
-        r.pa[j] = k <= r.hi - r.lo ? ga[k] : xf_zero();
-        r.pb[j] = k <= r.nhi - r.nlo ? gb[k] : xf_zero();
-      }
-    }
-    r.lgt = tid < D ? a.logits[((size_t)b * Imax + t) * D + tid] : 0.0f;
-  };
-  auto stage = [&](int t, const Rows& r) {
-    if (regs) {
-#pragma unroll
-      for (int j = 0; j < kF4GradPf; ++j) {
-        const int k = tid + kF4GradThreads * j;
-        if (k <= r.hi - r.lo) at[k] = r.pa[j];
-        if (k <= r.nhi - r.nlo) bn[k] = r.pb[j];
-      }
-    } else {
-      const xf* ga = W.alpha + ((size_t)b * (Imax + 1) + t) * Wc;
-      const xf* gb = W.beta + ((size_t)b * (Imax + 1) + t + 1) * Wc;
-      for (int k = tid; k <= r.hi - r.lo; k += kF4GradThreads) at[k] = ga[k];
-      for (int k = tid; k <= r.nhi - r.nlo; k += kF4GradThreads) bn[k] = gb[k];
-    }
-    if (tid == 0) at[Wc] = xf_zero();
-  };
-  auto step = [&](int t, const Rows& cur, Rows& nxt) {
-    stage(t, cur);
-    lds_sync();
-    if (t + 1 < tl) fetch(t + 1, nxt);  // in flight while step t sums
-    int lo = cur.lo;
-    const int hi = cur.hi, nlo = cur.nlo, nhi = cur.nhi;
-    const unsigned span = hi >= lo ? (unsigned)(hi - lo) : 0u;
-    if (hi < lo) lo = 1 << 29;  // empty alpha window: every offset out of range
-    xf acc[NCW];
-#pragma unroll
-    for (int j = 0; j < NCW; ++j) acc[j] = xf_zero();
-    for (int x = nlo + ((lane - nlo) & 63); x <= nhi; x += 64) {
-      const xf bv = bn[x - nlo];
-#pragma unroll
-      for (int j = 0; j < NCW; ++j) {
-        // a term outside the window is an exact zero: adding it leaves a normalized (or zero)
-        // partial unchanged, so the select is the oracle's skip
-        const unsigned yr = (unsigned)(x - di[j] - lo);
-        const xf av = at[yr <= span ? (int)yr : Wc];  // (zero cell: the oracle's skip)
-        acc[j] = xf_add(acc[j].m, acc[j].e, av.m * bv.m, av.e + bv.e);
-      }
-    }
-    // every class of this wave reduced at once; lane l < NCW then holds class cls (distinct)
-    const int cls = f4_reduce_classes<NCW>(acc, lane);
-    const int i = wave + cls * kF4GradWaves;
-    // one wave: the class log-prob of class i is held by thread i (one bpermute)
-    const float lgi = __shfl(cur.lgt, i & 63);
-    if (lane < NCW && i < D) {
-      const xf w = xf_exp(kF4GradWaves == 1 ? lgi : a.logits[((size_t)b * Imax + t) * D + i],
-                          a.allow_skip || i != a.zid);
-      a.grad[((size_t)b * Imax + t) * D + i] = xf_neg_post((acc[0].m * w.m) * izm, acc[0].e + w.e + ize);
-    }
-    lds_sync();  // (the rows of step t are read; the next stage overwrites them)
-  };
-  Rows r0, r1;  // alternating (no register copies of rows with loads in flight)
-  fetch(t0, r0);
-  for (int t = t0; t < tl; t += 2) {
-    step(t, r0, r1);
-    if (t + 1 < tl) step(t + 1, r1, r0);
+  // every class of this wave reduced at once; lane l < NCW then holds class cls (distinct)
+  const int cls = f4_reduce_classes<NCW>(acc, lane);
+  const int i = wave + cls * kF4GradWaves;
+  if (lane < NCW && i < D) {
+    const xf w = xf_exp(a.logits[((size_t)b * Imax + t) * D + i], a.allow_skip || i != a.zid);
+    g[i] = xf_neg_post((acc[0].m * w.m) * izm, acc[0].e + w.e + ize);
   }
 }
 
@@ -623,8 +562,7 @@ int launch_f4(const V2FwdBwdArgs& a, size_t lds, size_t glds, hipStream_t st) {
   if (glds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_f4_grad<DC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds);
-  hipLaunchKernelGGL(k_f4_grad<DC>, dim3(a.B, (a.Imax + kF4GradSteps) / kF4GradSteps),
-                     dim3(f4_grad_threads<DC>()), glds, st, a);
+  hipLaunchKernelGGL(k_f4_grad<DC>, dim3(a.B, a.Imax + 1), dim3(f4_grad_threads<DC>()), glds, st, a);
   return hipGetLastError() == hipSuccess ? SSNT_OK : SSNT_ERR_HIP;
 }
 
