@@ -15,7 +15,14 @@ sys.path.insert(0, str(ROOT / "ssnt-tts-rust_amd"))
 import ssnt_tts_amd as S  # noqa: E402
 
 B, T, U = 64, 2000, 400
-modes = [int(x) for x in sys.argv[1:]] or [0, 1, 2]
+# a form: "<split>" or "<split>k2" (two positions per lane: ssnt_fwd_bwd_wide_lanes(2))
+modes = sys.argv[1:] or ["0", "1", "2"]
+
+
+def set_form(ab, m):
+    assert ab.ssnt_fwd_bwd_wide_split(int(m[:-2] if m.endswith("k2") else m)) == 0
+    assert ab.ssnt_fwd_bwd_wide_lanes(2 if m.endswith("k2") else 1) == 0
+
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(4)
 lt = torch.log_softmax(torch.randn((B, T, U, 2), device=dev, generator=g) * 1.5, -1).contiguous()
@@ -26,7 +33,7 @@ kern = {}
 with S.use_ab() as ab:
     ref = None
     for m in modes:
-        assert ab.ssnt_fwd_bwd_wide_split(m) == 0
+        set_form(ab, m)
         r = S.ssnt_fwd_bwd(lt, sl, pl, check=True)
         kern[m] = S.last_fwd_bwd_kernel()
         got = (r["loss"].cpu(), r["grad"].cpu())
@@ -39,7 +46,7 @@ with S.use_ab() as ab:
            "status": torch.zeros(1, dtype=torch.int32, device=dev)}
     for _ in range(5):
         for m in modes:
-            ab.ssnt_fwd_bwd_wide_split(m)
+            set_form(ab, m)
             S.ssnt_fwd_bwd(lt, sl, pl, out=out)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,4 +57,4 @@ with S.use_ab() as ab:
             torch.cuda.synchronize()
             times[m].append(e0.elapsed_time(e1) / 4 * 1e3)
 for m in modes:
-    print(json.dumps({"split_mode": m, "kernel": kern[m], "us": round(float(np.median(times[m])), 1)}))
+    print(json.dumps({"form": m, "kernel": kern[m], "us": round(float(np.median(times[m])), 1)}))
