@@ -57,11 +57,17 @@ template <int K, int PHASE, bool SPLIT>
 constexpr int block_steps() {
   return K == 1 ? (PHASE == 1 ? (SPLIT ? 32 : 16) : 16) : 8;
 }
-constexpr int kRB = 64;        // hand-off ring slots (steps) per wave
+// hand-off ring slots (steps) per wave: 64 in one workgroup; 128 when a direction is split, so
+// that the global hand-off moves 64 steps per publication (kPub; 16-step publications made the
+// split form slower than one workgroup, 64 made it faster: DESIGN.md 5.2 round 5)
+template <bool SPLIT>
+constexpr int ring_slots() { return SPLIT ? 128 : 64; }
+constexpr int kPub = 64;       // steps per global publication (SPLIT)
 constexpr int kMaxNW = 8;      // waves per direction: U <= 512 (K = 1) / 1024 (K = 2)
 constexpr int kProxy = kMaxNW; // ring / counter index of the proxy wave (SPLIT)
 constexpr int kSpinMax = 1 << 22;
 
+template <int kRB>
 struct WideCtl {
   int prod[kMaxNW + 1];     // steps whose hand-off value ring w holds (w = kProxy: the receiver's)
   int cons[kMaxNW + 1];     // steps of its upstream ring wave w has read (kProxy: the publisher)
@@ -163,9 +169,10 @@ template <int K, bool OBS, int PHASE, bool DBG, bool SPLIT>
 __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k_fwd_bwd_wide(FwdBwdArgs a, WideGrid gd) {
   constexpr int kSeg = 64 * K;
   constexpr int kBS = block_steps<K, PHASE, SPLIT>();
+  constexpr int kRB = ring_slots<SPLIT>();
   static_assert(kRB % kBS == 0, "hand-off blocks must tile the ring");
   constexpr int kDepth = kBS;  // rows in flight per wave
-  __shared__ WideCtl ctl;
+  __shared__ WideCtl<kRB> ctl;
   int b, dir, part;  // dir 0 alpha, 1 beta; part 0 upstream, 1 downstream (SPLIT)
   if constexpr (SPLIT) {
     const int id = blockIdx.x;
@@ -407,20 +414,29 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
 
   // SPLIT proxies (header): n steps of hand-off, kBS values per block, 16 B per lane
   auto run_proxy = [&](int n) __attribute__((always_inline)) {
-    constexpr int kL = kBS / 2;
+    // hand-off granule: kPub steps (2 - 4 blocks) per global publication
+    constexpr int kPB = kPub;
+    static_assert(kRB % kPB == 0, "publication granules tile the ring");
+    constexpr int kL = kPB / 4;  // lanes moving the granule, 32 B (4 xf) each
     const __amdgpu_buffer_rsrc_t gr = brsrc(gd.gring + (size_t)(b * 2 + dir) * gd.RL, gd.RL * 8u);
     int* ctr = gd.ctr + ((PHASE - 1) * a.B + b) * 2 + dir;
     if (part == 0) {  // publisher: the last compute wave's ring -> global
       const int src = ncomp - 1;
-      for (int i0 = 0; i0 < n; i0 += kBS) {
-        const int i1 = min(i0 + kBS, n);
+      for (int i0 = 0; i0 < n; i0 += kPB) {
+        const int i1 = min(i0 + kPB, n);
         wait_ge(&ctl.prod[src], i1, a.status);
         wbar();
-        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (lane < kL) v = *reinterpret_cast<const f32x4*>(&ctl.bnd[src][i0 % kRB + 2 * lane]);
+        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f}, v2 = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (lane < kL) {
+          v = *reinterpret_cast<const f32x4*>(&ctl.bnd[src][i0 % kRB + 4 * lane]);
+          v2 = *reinterpret_cast<const f32x4*>(&ctl.bnd[src][i0 % kRB + 4 * lane + 2]);
+        }
         wbar();
-        wctr_st(&ctl.cons[kProxy], i1);  // (DS in order: the read above is done first)
-        if (lane < kL) rbuf_st4(v, gr, (i0 + 2 * lane) * 8, 0, kSC1);
+        wctr_st(&ctl.cons[kProxy], i1);  // (DS in order: the reads above are done first)
+        if (lane < kL) {
+          rbuf_st4(v, gr, (i0 + 4 * lane) * 8, 0, kSC1);
+          rbuf_st4(v2, gr, (i0 + 4 * lane + 2) * 8, 0, kSC1);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores only
         if (lane == 0) __hip_atomic_store(ctr, i1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -428,19 +444,28 @@ __global__ __launch_bounds__(SPLIT ? 64 * (kMaxNW / 2 + 1) : 64 * kMaxNW) void k
       int seen = 0;
       bool dead = false;  // the upstream workgroup never published: forward NaN from here on, so
                           // the utterance's loss and gradients are NaN, never plausible values
-      for (int i0 = 0; i0 < n; i0 += kBS) {
-        const int i1 = min(i0 + kBS, n);
+      for (int i0 = 0; i0 < n; i0 += kPB) {
+        const int i1 = min(i0 + kPB, n);
         if (!dead && seen < i1) {
           seen = gwait_ge(ctr, i1, a.status);
           dead = seen < 0;
         }
         asm volatile("" ::: "memory");  // the payload loads stay behind the poll
-        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (lane < kL) v = rbuf_ld4(gr, (i0 + 2 * lane) * 8, 0, kSC1);
-        if (dead) v = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f}, v2 = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (lane < kL) {
+          v = rbuf_ld4(gr, (i0 + 4 * lane) * 8, 0, kSC1);
+          v2 = rbuf_ld4(gr, (i0 + 4 * lane + 2) * 8, 0, kSC1);
+        }
+        if (dead) {
+          v = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+          v2 = v;
+        }
         wait_ge(&ctl.cons[0], i1 - kRB, a.status);
         wbar();
-        if (lane < kL) *reinterpret_cast<f32x4*>(&ctl.bnd[kProxy][i0 % kRB + 2 * lane]) = v;
+        if (lane < kL) {
+          *reinterpret_cast<f32x4*>(&ctl.bnd[kProxy][i0 % kRB + 4 * lane]) = v;
+          *reinterpret_cast<f32x4*>(&ctl.bnd[kProxy][i0 % kRB + 4 * lane + 2]) = v2;
+        }
         wbar();
         wctr_st(&ctl.prod[kProxy], i1);
       }
@@ -817,10 +842,9 @@ inline WideLayout wide_layout(int B, int T, int U) {
   return l;
 }
 
-// -1 auto (default): split when the unsplit grid would leave most CUs idle (8B <= CUs) or for
-// the heaviest workgroups (K = 2, 8 waves) when 4B <= CUs -- measured per shape, DESIGN.md 5.2
-// (configs[4], B=64 U=400: one workgroup 604 vs split 637 us; B=32: 565 vs 511; B=64 U=1024:
-// 868 vs 749); 0 never; 1 whenever NW >= 2; 2 (A/B study) phase 2 only
+// -1 auto (default): split when the unsplit grid would leave most CUs idle (8B <= CUs), or when
+// the split grid fits the chip (4B <= CUs) and the lattice is long (T >= 640) -- measured per
+// shape; 0 never; 1 whenever NW >= 2; 2 (A/B study) phase 2 only
 #ifdef SSNT_AB
 std::atomic<int> g_wide_split{-1};  // A/B build: ssnt_fwd_bwd_wide_split
 int wide_split_mode() { return g_wide_split.load(std::memory_order_relaxed); }
@@ -858,7 +882,11 @@ int launch_wide(const FwdBwdArgs& a, hipStream_t st) {
     split = true;
   } else if (NW >= 2 && mode == -1) {
     const int cus = device_cus();
-    split = 8 * a.B <= cus || (K == 2 && NW == kMaxNW && 4 * a.B <= cus);
+    // (round 5, 64-step publications: lattices of T >= 640 split whenever the split grid still
+    // fits the chip -- configs[4] B=64 T=2000 U=400 539 vs 585 us, T=760 U=700 399 vs 496,
+    // T=1100 U=1024 671 vs 867; at T=400 U=300 the one-workgroup form stays ahead, 132 vs 154;
+    // profiles/r5i_split_shapes.jsonl)
+    split = 8 * a.B <= cus || (4 * a.B <= cus && a.T >= 640);
   }
   if (NW >= 2 && mode == 2) {  // A/B study: phase 1 in one workgroup per direction, phase 2 split
     if (hipMemsetAsync(gd.ctr, 0, l.ctr, st) != hipSuccess) return SSNT_ERR_HIP;

@@ -14,9 +14,11 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "ssnt-tts-rust_amd"))
 import ssnt_tts_amd as S  # noqa: E402
 
-B, T, U = 64, 2000, 400
-# a form: "<split>" or "<split>k2" (two positions per lane: ssnt_fwd_bwd_wide_lanes(2))
-modes = sys.argv[1:] or ["0", "1", "2"]
+# args: [B T U] form... -- a form is "<split>" or "<split>k2" (two positions per lane:
+# ssnt_fwd_bwd_wide_lanes(2)); default configs[4] and forms 0 1 2
+args = sys.argv[1:]
+B, T, U = (int(x) for x in args[:3]) if len(args) >= 3 and int(args[0]) > 2 else (64, 2000, 400)
+modes = (args[3:] if len(args) >= 3 and int(args[0]) > 2 else args) or ["0", "1", "2"]
 
 
 def set_form(ab, m):
@@ -57,4 +59,5 @@ with S.use_ab() as ab:
             torch.cuda.synchronize()
             times[m].append(e0.elapsed_time(e1) / 4 * 1e3)
 for m in modes:
-    print(json.dumps({"form": m, "kernel": kern[m], "us": round(float(np.median(times[m])), 1)}))
+    print(json.dumps({"B": B, "T": T, "U": U, "form": m, "kernel": kern[m],
+                      "us": round(float(np.median(times[m])), 1)}))
