@@ -184,6 +184,20 @@ def test_debug64_north_star_tolerance(gpu, oracle, kernel_variant, config):
     print(config, gpu.last_fwd_bwd_kernel(), worst)
 
 
+def test_debug64_all_config5_utterances(gpu, oracle, kernel_variant):
+    # every one of the 64 configs[4] utterances (B=64 T=2000 U=400, the seed of the long-form
+    # parity test) through the product dispatch: float64 log-alpha / log-beta / loss within the
+    # north_star 1e-5 abs of the float64 DP (CPU study: 8.7e-6 at worst)
+    if kernel_variant != 0:
+        pytest.skip("the product's own dispatch")
+    B, T, U = 64, 2000, 400
+    lt = oracle.synth_log_trans(B, T, U, seed=4)
+    S, P = [T] * B, [U] * B
+    g = _run_debug64(gpu, lt, S, P)
+    worst = _check_debug64(g, lt, S, P, oracle)
+    print("configs4_all_64", gpu.last_fwd_bwd_kernel(), worst)
+
+
 @pytest.mark.parametrize("flags", [F_TERM, 0, F_TERM | F_ZINF])
 def test_debug64_ragged_and_edges(gpu, oracle, kernel_variant, flags):
     # infeasible (loss +inf / 0 with zero_infinity, every row -inf), single cell, S == P, log(0)
