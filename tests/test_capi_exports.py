@@ -110,7 +110,7 @@ def test_mirror_fails_loudly_without_gpu():
 def test_segmented_workspace_query_covers_the_handoff_block():
     # host-only queries (no HIP call): the long-row kernel's workspace = the hand-off counter
     # block + the global hand-off rings + its rows (fwd_bwd_wide.hip wide_layout), each piece
-    # padded to 256 B; the A/B build's hook for its workgroup split takes -1 / 0 / 1 only
+    # padded to 256 B; the A/B build's hook for its workgroup split takes -1 / 0 / 1 / 2 only
     from ssnt_tts_amd._lib import load, load_ab
     lib = load()
     r256 = lambda x: (x + 255) & ~255  # noqa: E731
@@ -119,7 +119,7 @@ def test_segmented_workspace_query_covers_the_handoff_block():
         stream = B * T * (U + 3) * 8
         assert lib.ssnt_fwd_bwd_workspace_size(B, T, U) == max(wide, stream), (B, T, U)
     ab = load_ab()
-    for bad in (-2, 2, 7):
+    for bad in (-2, 3, 7):
         assert ab.ssnt_fwd_bwd_wide_split(bad) != 0
-    for ok in (0, 1, -1):
+    for ok in (0, 1, 2, -1):
         assert ab.ssnt_fwd_bwd_wide_split(ok) == 0
